@@ -1,0 +1,127 @@
+/*
+ * zkalgebra_gpu.h -- C ABI of the MI355X (gfx950) MSM / NTT library.
+ *
+ * Part 1 exports EXACTLY the symbols and signatures of the reference's generated C
+ * that its Haskell FFI modules bind with `foreign import ccall unsafe` (drop-in
+ * boundary).  Part 2 adds device-resident and helper entry points that
+ * the reference does not have (benchmarking, multi-GPU sharding, input generation).
+ *
+ * Layouts (identical to the reference, Class/Flat.hs:81-83):
+ *   u64 little-endian limbs; Fr = 4 limbs; Fp = 4 (bn128) or 6 (bls12_381) limbs;
+ *   affine G1 = x || y (Montgomery Fp), infinity = all bytes 0xFF;
+ *   projective G1 = X || Y || Z (x = X/Z, y = Y/Z), Jacobian = X || Y || Z (x = X/Z^2).
+ * All buffers are caller-owned and are not retained after the call returns.
+ * Every call is synchronous and thread-safe.  There are no error codes on the
+ * reference ABI: on a device error the library prints a message and aborts (the
+ * reference asserts, bls12_381_G1_proj.c:518,632) -- it never falls back to a CPU path.
+ *
+ * Projective / Jacobian outputs are returned NORMALISED (Z = 1, or the canonical
+ * infinity (0:1:0) / Jacobian (1:1:0)); they are equal as points to the reference's
+ * un-normalised outputs (whose exact coordinates depend on its operation order and
+ * are not reproducible).  Affine outputs are bit-identical.
+ */
+#ifndef ZKALGEBRA_GPU_H
+#define ZKALGEBRA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZKG_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------------
+ * Part 1: reference symbols.  <C> in {bn128, bls12_381}.
+ * ---------------------------------------------------------------------------- */
+
+/* MSM, G1, homogeneous projective.
+ *   lib/cbits/curves/g1/proj/bls12_381_G1_proj.h:43-46 (bn128_G1_proj.h same lines)
+ *   mont_coeff_proj_out  <- Haskell `msm`    (lib/src/ZK/Algebra/Curves/<C>/G1/Proj.hs:229,245)
+ *   std_coeff_proj_out   <- Haskell `msmStd` (G1/Proj.hs:228,262)
+ *   _affine_out          <- bls12_381_G1_proj.c:654-670
+ *   expos: npoints x expo_nlimbs u64 (Montgomery Fr for mont_coeff, plain integers for
+ *   std_coeff, used verbatim -- no reduction mod r).  expo_nlimbs: 4 (mont), 1..4 (std).
+ *   grps : npoints affine points.  tgt: 3*NP (proj) or 2*NP (affine) u64. */
+ZKG_API void bn128_G1_proj_MSM_mont_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G1_proj_MSM_std_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G1_proj_MSM_mont_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G1_proj_MSM_std_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+/* bn128_G1_proj.c:506 -- window_size is honoured as the GPU window (clamped to [4,24]) */
+ZKG_API void bn128_G1_proj_MSM_std_coeff_proj_out_variable(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs, int window_size);
+
+ZKG_API void bls12_381_G1_proj_MSM_mont_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G1_proj_MSM_std_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G1_proj_MSM_mont_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G1_proj_MSM_std_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+/* bls12_381_G1_proj.c:507 */
+ZKG_API void bls12_381_G1_proj_MSM_std_coeff_proj_out_variable(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs, int window_size);
+
+/* MSM, G1, Jacobian output (secondary; bls12_381_G1_jac.h:43-46, bound by G1/Jac.hs:225-226) */
+ZKG_API void bn128_G1_jac_MSM_std_coeff_jac_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G1_jac_MSM_mont_coeff_jac_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G1_jac_MSM_std_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G1_jac_MSM_mont_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G1_jac_MSM_std_coeff_jac_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G1_jac_MSM_mont_coeff_jac_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G1_jac_MSM_std_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G1_jac_MSM_mont_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+
+/* NTT over Fr, natural order in/out, 2^m elements, gen = Montgomery generator of the
+ * order-2^m subgroup (Haskell passes fftSubgroupGen).  Out-of-place.
+ *   lib/cbits/curves/poly/mont/bls12_381_poly_mont.h:27-28 (bn128_poly_mont.h same)
+ *   forward <- Haskell forwardNTT (lib/src/ZK/Algebra/Curves/<C>/Poly.hs:397,409)
+ *   inverse <- Haskell inverseNTT (Poly.hs:398,421) */
+ZKG_API void bn128_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
+ZKG_API void bn128_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
+ZKG_API void bls12_381_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
+ZKG_API void bls12_381_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
+
+/* ------------------------------------------------------------------------------
+ * Part 2: extensions (not in the reference).  curve: 0 = bn128, 1 = bls12_381.
+ * ---------------------------------------------------------------------------- */
+#define ZKG_BN128 0
+#define ZKG_BLS12_381 1
+
+ZKG_API const char *zkg_version(void);
+ZKG_API int zkg_device_count(void);
+ZKG_API void zkg_set_device(int device);           /* binds the calling thread */
+ZKG_API void *zkg_device_malloc(size_t bytes);
+ZKG_API void zkg_device_free(void *ptr);
+ZKG_API void zkg_memcpy_htod(void *dst, const void *src, size_t bytes);
+ZKG_API void zkg_memcpy_dtoh(void *dst, const void *src, size_t bytes);
+ZKG_API void zkg_device_synchronize(void);
+
+/* device-resident MSM: d_expos / d_grps are DEVICE pointers (already in HBM);
+ * tgt_proj is a HOST buffer of 3*NP u64 receiving the normalised projective sum. */
+ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,
+                               const uint64_t *d_grps, uint64_t *tgt_proj, int window_size);
+/* device-resident NTT: d_src / d_tgt DEVICE pointers; gen on the host */
+ZKG_API void zkg_ntt_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src, uint64_t *d_tgt);
+
+/* host helpers on G1 (projective, reference Montgomery form) */
+ZKG_API void zkg_g1_proj_add(int curve, const uint64_t *a, const uint64_t *b, uint64_t *out);
+ZKG_API void zkg_g1_proj_normalize(int curve, const uint64_t *a, uint64_t *out);
+ZKG_API void zkg_g1_proj_to_affine(int curve, const uint64_t *a, uint64_t *out);
+
+/* deterministic synthetic inputs (spec: zikkurat-algebra_amd/csrc/zk_gen.cpp) */
+ZKG_API void zkg_gen_fr(int curve, uint64_t seed, int64_t start, int64_t count, uint64_t *out);
+ZKG_API void zkg_gen_g1_points(int curve, uint64_t seed, int64_t start, int64_t count, uint64_t *out);
+/* Montgomery generator of the order-2^m subgroup: fftDomain gen^(2^(M-m))
+ * (Class/FFT.hs:60-66; BLS12_381/Fr/Mont.hs:145-151, BN128/Fr/Mont.hs:146-148) */
+ZKG_API void zkg_fft_generator(int curve, int m, uint64_t *out);
+
+/* MSM window heuristic used when window_size is not given */
+ZKG_API int zkg_msm_default_window(int npoints);
+
+/* timing probe of the dominant kernel (MSM bucket accumulation / NTT pass chain),
+ * measured with HIP events on the library's own stream */
+ZKG_API void zkg_timer_enable(int on);
+ZKG_API void zkg_timer_reset(void);
+ZKG_API void zkg_timer_read(double *total_ms, long *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZKALGEBRA_GPU_H */

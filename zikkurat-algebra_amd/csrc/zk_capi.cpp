@@ -1,0 +1,252 @@
+// zk_capi.cpp -- the extern "C" boundary (include/zkalgebra_gpu.h).
+//
+// Part 1 mirrors the reference's generated C entry points one for one:
+//   <C>_G1_proj_MSM_{mont,std}_coeff_{proj,affine}_out  bls12_381_G1_proj.c:597-670
+//   <C>_G1_proj_MSM_std_coeff_proj_out_variable          bls12_381_G1_proj.c:507
+//   <C>_G1_jac_MSM_{mont,std}_coeff_{jac,affine}_out    bls12_381_G1_jac.c:555-718
+//   <C>_poly_mont_ntt_{forward,inverse}                  bls12_381_poly_mont.c:457,516
+// Every one of them runs on the GPU; there is no CPU fallback path.
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include "../../include/zkalgebra_gpu.h"
+#include "zk_gen.hpp"
+#include "zk_host.hpp"
+#include "zk_msm.hpp"
+#include "zk_ntt.hpp"
+#include "zk_runtime.hpp"
+
+using namespace zk;
+
+namespace {
+
+enum Out { PROJ, AFFINE, JAC };
+
+template <class C>
+void msm_entry(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int nl, bool mont,
+               int window, Out out) {
+  using HF = typename HostOf<C>::Fp;
+  constexpr int NP = C::NP64;
+  uint64_t proj[3 * NP];
+  msm_g1<C>(npoints, expos, nl, grps, /*host_inputs=*/true, mont, window, proj);
+  zkh::Proj<HF> p;
+  memcpy(p.X.v, proj, NP * 8);
+  memcpy(p.Y.v, proj + NP, NP * 8);
+  memcpy(p.Z.v, proj + 2 * NP, NP * 8);
+  if (out == AFFINE) {
+    zkh::Aff<HF> a;
+    zkh::proj_to_aff(a, p);
+    memcpy(tgt, a.x.v, NP * 8);
+    memcpy(tgt + NP, a.y.v, NP * 8);
+    return;
+  }
+  zkh::Proj<HF> q;
+  zkh::proj_normalize(q, p);
+  if (out == JAC && zkh::proj_is_inf(q)) zkh::set_one(q.X);  // Jacobian infinity (1:1:0), G1_jac.c:183-187
+  memcpy(tgt, q.X.v, NP * 8);
+  memcpy(tgt + NP, q.Y.v, NP * 8);
+  memcpy(tgt + 2 * NP, q.Z.v, NP * 8);
+}
+
+template <class HF, class C>
+void host_b3(zkh::Fe<HF> &b3) { HostOf<C>::b3(b3); }
+
+}  // namespace
+
+extern "C" {
+
+#define ZKG_MSM_ENTRIES(PFX, CURVE)                                                                             \
+  ZKG_API void PFX##_G1_proj_MSM_mont_coeff_proj_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,  \
+                                                     int nl) {                                                  \
+    msm_entry<CURVE>(n, e, g, t, nl, true, 0, PROJ);                                                           \
+  }                                                                                                             \
+  ZKG_API void PFX##_G1_proj_MSM_std_coeff_proj_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,   \
+                                                    int nl) {                                                   \
+    msm_entry<CURVE>(n, e, g, t, nl, false, 0, PROJ);                                                          \
+  }                                                                                                             \
+  ZKG_API void PFX##_G1_proj_MSM_mont_coeff_affine_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t, \
+                                                       int nl) {                                                \
+    msm_entry<CURVE>(n, e, g, t, nl, true, 0, AFFINE);                                                         \
+  }                                                                                                             \
+  ZKG_API void PFX##_G1_proj_MSM_std_coeff_affine_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,  \
+                                                      int nl) {                                                 \
+    msm_entry<CURVE>(n, e, g, t, nl, false, 0, AFFINE);                                                        \
+  }                                                                                                             \
+  ZKG_API void PFX##_G1_proj_MSM_std_coeff_proj_out_variable(int n, const uint64_t *e, const uint64_t *g,       \
+                                                             uint64_t *t, int nl, int window) {                 \
+    int c = window < 4 ? 4 : (window > 24 ? 24 : window);                                                       \
+    msm_entry<CURVE>(n, e, g, t, nl, false, c, PROJ);                                                          \
+  }                                                                                                             \
+  ZKG_API void PFX##_G1_jac_MSM_std_coeff_jac_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,     \
+                                                  int nl) {                                                     \
+    msm_entry<CURVE>(n, e, g, t, nl, false, 0, JAC);                                                           \
+  }                                                                                                             \
+  ZKG_API void PFX##_G1_jac_MSM_mont_coeff_jac_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,    \
+                                                   int nl) {                                                    \
+    msm_entry<CURVE>(n, e, g, t, nl, true, 0, JAC);                                                            \
+  }                                                                                                             \
+  ZKG_API void PFX##_G1_jac_MSM_std_coeff_affine_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,  \
+                                                     int nl) {                                                  \
+    msm_entry<CURVE>(n, e, g, t, nl, false, 0, AFFINE);                                                        \
+  }                                                                                                             \
+  ZKG_API void PFX##_G1_jac_MSM_mont_coeff_affine_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t, \
+                                                      int nl) {                                                 \
+    msm_entry<CURVE>(n, e, g, t, nl, true, 0, AFFINE);                                                         \
+  }
+
+ZKG_MSM_ENTRIES(bn128, BN254)
+ZKG_MSM_ENTRIES(bls12_381, BLS381)
+
+ZKG_API void bn128_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
+  zk::ntt(ZKG_BN128, m, gen, src, tgt, true, false);
+}
+ZKG_API void bn128_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
+  zk::ntt(ZKG_BN128, m, gen, src, tgt, true, true);
+}
+ZKG_API void bls12_381_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
+  zk::ntt(ZKG_BLS12_381, m, gen, src, tgt, true, false);
+}
+ZKG_API void bls12_381_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
+  zk::ntt(ZKG_BLS12_381, m, gen, src, tgt, true, true);
+}
+
+// ---------------------------------------------------------------------------- Part 2
+
+ZKG_API const char *zkg_version(void) { return "zkalgebra_gpu 0.1 (gfx950)"; }
+
+ZKG_API int zkg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+ZKG_API void zkg_set_device(int device) { ZK_CHECK(hipSetDevice(device)); }
+ZKG_API void *zkg_device_malloc(size_t bytes) {
+  void *p = nullptr;
+  ZK_CHECK(hipMalloc(&p, bytes ? bytes : 1));
+  return p;
+}
+ZKG_API void zkg_device_free(void *ptr) {
+  if (ptr) ZK_CHECK(hipFree(ptr));
+}
+ZKG_API void zkg_memcpy_htod(void *dst, const void *src, size_t bytes) {
+  ZK_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+}
+ZKG_API void zkg_memcpy_dtoh(void *dst, const void *src, size_t bytes) {
+  ZK_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+}
+ZKG_API void zkg_device_synchronize(void) { ZK_CHECK(hipDeviceSynchronize()); }
+
+ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,
+                               const uint64_t *d_grps, uint64_t *tgt_proj, int window_size) {
+  int c = window_size <= 0 ? 0 : (window_size < 4 ? 4 : (window_size > 24 ? 24 : window_size));
+  if (curve == ZKG_BN128) {
+    uint64_t p[12];
+    msm_g1<BN254>(npoints, d_expos, expo_nlimbs, d_grps, false, expos_mont != 0, c, p);
+    zkg_g1_proj_normalize(curve, p, tgt_proj);
+  } else {
+    uint64_t p[18];
+    msm_g1<BLS381>(npoints, d_expos, expo_nlimbs, d_grps, false, expos_mont != 0, c, p);
+    zkg_g1_proj_normalize(curve, p, tgt_proj);
+  }
+}
+
+ZKG_API void zkg_ntt_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src,
+                            uint64_t *d_tgt) {
+  zk::ntt(curve, m, gen, d_src, d_tgt, false, inverse != 0);
+}
+
+}  // extern "C"
+
+template <class C>
+static void proj_op(int op, const uint64_t *a, const uint64_t *b, uint64_t *out) {
+  using HF = typename HostOf<C>::Fp;
+  constexpr int NP = C::NP64;
+  zkh::Proj<HF> p, q, r;
+  memcpy(p.X.v, a, NP * 8);
+  memcpy(p.Y.v, a + NP, NP * 8);
+  memcpy(p.Z.v, a + 2 * NP, NP * 8);
+  if (op == 0) {
+    memcpy(q.X.v, b, NP * 8);
+    memcpy(q.Y.v, b + NP, NP * 8);
+    memcpy(q.Z.v, b + 2 * NP, NP * 8);
+    zkh::Fe<HF> b3;
+    HostOf<C>::b3(b3);
+    zkh::proj_add(r, p, q, b3);
+  } else if (op == 1) {
+    zkh::proj_normalize(r, p);
+  } else {
+    zkh::Aff<HF> af;
+    zkh::proj_to_aff(af, p);
+    memcpy(out, af.x.v, NP * 8);
+    memcpy(out + NP, af.y.v, NP * 8);
+    return;
+  }
+  memcpy(out, r.X.v, NP * 8);
+  memcpy(out + NP, r.Y.v, NP * 8);
+  memcpy(out + 2 * NP, r.Z.v, NP * 8);
+}
+
+extern "C" {
+
+ZKG_API void zkg_g1_proj_add(int curve, const uint64_t *a, const uint64_t *b, uint64_t *out) {
+  if (curve == ZKG_BN128) proj_op<BN254>(0, a, b, out); else proj_op<BLS381>(0, a, b, out);
+}
+ZKG_API void zkg_g1_proj_normalize(int curve, const uint64_t *a, uint64_t *out) {
+  if (curve == ZKG_BN128) proj_op<BN254>(1, a, nullptr, out); else proj_op<BLS381>(1, a, nullptr, out);
+}
+ZKG_API void zkg_g1_proj_to_affine(int curve, const uint64_t *a, uint64_t *out) {
+  if (curve == ZKG_BN128) proj_op<BN254>(2, a, nullptr, out); else proj_op<BLS381>(2, a, nullptr, out);
+}
+
+ZKG_API void zkg_gen_fr(int curve, uint64_t seed, int64_t start, int64_t count, uint64_t *out) {
+  if (curve == ZKG_BN128) zkg::gen_field<zkh::BN_Fr>(seed, start, count, out);
+  else zkg::gen_field<zkh::BLS_Fr>(seed, start, count, out);
+}
+
+ZKG_API void zkg_gen_g1_points(int curve, uint64_t seed, int64_t start, int64_t count, uint64_t *out) {
+  if (curve == ZKG_BN128) {
+    const uint64_t gx[] = ZK_BN128_GX_FP64, gy[] = ZK_BN128_GY_FP64, b3[] = ZK_BN128_B3_FP64;
+    zkg::gen_points<zkh::BN_Fp, zkh::BN_Fr>(seed, start, count, out, gx, gy, b3);
+  } else {
+    const uint64_t gx[] = ZK_BLS12_381_GX_FP64, gy[] = ZK_BLS12_381_GY_FP64, b3[] = ZK_BLS12_381_B3_FP64;
+    zkg::gen_points<zkh::BLS_Fp, zkh::BLS_Fr>(seed, start, count, out, gx, gy, b3);
+  }
+}
+
+ZKG_API void zkg_fft_generator(int curve, int m, uint64_t *out) {
+  if (curve == ZKG_BN128) {
+    zkh::Fe<zkh::BN_Fr> g;
+    const uint64_t v[] = ZK_BN128_FFT_GEN_FR64;
+    memcpy(g.v, v, sizeof g.v);
+    for (int i = m; i < ZK_BN128_FFT_LOG; i++) zkh::sqr(g, g);
+    memcpy(out, g.v, sizeof g.v);
+  } else {
+    zkh::Fe<zkh::BLS_Fr> g;
+    const uint64_t v[] = ZK_BLS12_381_FFT_GEN_FR64;
+    memcpy(g.v, v, sizeof g.v);
+    for (int i = m; i < ZK_BLS12_381_FFT_LOG; i++) zkh::sqr(g, g);
+    memcpy(out, g.v, sizeof g.v);
+  }
+}
+
+ZKG_API int zkg_msm_default_window(int npoints) { return zk::msm_default_window(npoints); }
+
+ZKG_API void zkg_timer_enable(int on) {
+  KernelTimer &t = dominant_timer();
+  if (on && !t.ev0) {
+    ZK_CHECK(hipEventCreate(&t.ev0));
+    ZK_CHECK(hipEventCreate(&t.ev1));
+  }
+  t.enabled = on != 0;
+}
+ZKG_API void zkg_timer_reset(void) {
+  KernelTimer &t = dominant_timer();
+  t.total_ms = 0;
+  t.launches = 0;
+}
+ZKG_API void zkg_timer_read(double *total_ms, long *launches) {
+  KernelTimer &t = dominant_timer();
+  if (total_ms) *total_ms = t.total_ms;
+  if (launches) *launches = t.launches;
+}
+
+}  // extern "C"

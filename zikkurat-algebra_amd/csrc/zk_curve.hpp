@@ -1,0 +1,182 @@
+// zk_curve.hpp -- G1 point arithmetic on the device, short Weierstrass a = 0.
+//
+// The reference accumulates buckets in homogeneous projective coordinates with the
+// madd-1998-cmo mixed add (bls12_381_G1_proj.c:334-374, 9M+2S) and the complete
+// add-2015-rcb (:273-314, 12M).  On the GPU the bucket accumulators are kept in
+// extended Jacobian "XYZZ" coordinates (x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2), whose
+// mixed add is 8M+2S and whose special cases (P == Q, P == -Q, infinity) are cheap
+// to detect.  Only the affine / normalised result leaves the device, and that is
+// canonical, so the coordinate system is invisible at the C ABI.
+//
+// Affine input points use the reference's encoding: Montgomery x || y with the point at
+// infinity as all-0xFF bytes (bls12_381_G1_affine.c:1-6, :63-66).
+#pragma once
+#include "zk_field.hpp"
+
+namespace zk {
+
+// curve descriptors: base field, scalar field, and the constants we need
+struct BN254 {
+  using Fp = BN_Fp;
+  using Fr = BN_Fr;
+  static constexpr int NP64 = ZK_BN128_FP_N64;
+};
+struct BLS381 {
+  using Fp = BLS_Fp;
+  using Fr = BLS_Fr;
+  static constexpr int NP64 = ZK_BLS12_381_FP_N64;
+};
+
+template <class F>
+struct Aff {
+  Fe<F> x, y;
+};
+// XYZZ with infinity encoded as ZZ == 0
+template <class F>
+struct Xyzz {
+  Fe<F> X, Y, ZZ, ZZZ;
+};
+
+template <class F>
+__device__ __forceinline__ void xyzz_set_inf(Xyzz<F> &r) {
+  fe_one(r.X);
+  fe_one(r.Y);
+  fe_zero(r.ZZ);
+  fe_zero(r.ZZZ);
+}
+template <class F>
+__device__ __forceinline__ bool xyzz_is_inf(const Xyzz<F> &a) {
+  return fe_is_zero(a.ZZ);
+}
+template <class F>
+__device__ __forceinline__ void xyzz_from_aff(Xyzz<F> &r, const Aff<F> &a) {
+  r.X = a.x;
+  r.Y = a.y;
+  fe_one(r.ZZ);
+  fe_one(r.ZZZ);
+}
+
+// r = 2*(x, y) for an affine point (mdbl-2008-s-1), result XYZZ
+template <class F>
+__device__ __forceinline__ void xyzz_dbl_aff(Xyzz<F> &r, const Aff<F> &a) {
+  Fe<F> U, V, W, S, M, t;
+  fe_add(U, a.y, a.y);     // U = 2Y
+  fe_sqr(V, U);            // V = U^2
+  fe_mul(W, U, V);         // W = U*V
+  fe_mul(S, a.x, V);       // S = X*V
+  fe_sqr(t, a.x);
+  fe_mul3(M, t);           // M = 3X^2
+  fe_sqr(t, M);
+  fe_sub(t, t, S);
+  fe_sub(r.X, t, S);       // X3 = M^2 - 2S
+  fe_sub(t, S, r.X);
+  fe_mul(t, M, t);
+  fe_mul(U, W, a.y);
+  fe_sub(r.Y, t, U);       // Y3 = M(S - X3) - W*Y
+  r.ZZ = V;
+  r.ZZZ = W;
+}
+
+// r = 2*p (dbl-2008-s-1), XYZZ
+template <class F>
+__device__ __forceinline__ void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &p) {
+  if (xyzz_is_inf(p)) { r = p; return; }
+  Fe<F> U, V, W, S, M, t;
+  fe_add(U, p.Y, p.Y);
+  fe_sqr(V, U);
+  fe_mul(W, U, V);
+  fe_mul(S, p.X, V);
+  fe_sqr(t, p.X);
+  fe_mul3(M, t);
+  fe_sqr(t, M);
+  fe_sub(t, t, S);
+  Fe<F> X3;
+  fe_sub(X3, t, S);
+  fe_sub(t, S, X3);
+  fe_mul(t, M, t);
+  fe_mul(U, W, p.Y);
+  fe_sub(r.Y, t, U);
+  r.X = X3;
+  fe_mul(r.ZZ, V, p.ZZ);
+  fe_mul(r.ZZZ, W, p.ZZZ);
+}
+
+// acc += a  (mixed add, madd-2008-s), all special cases handled
+template <class F>
+__device__ __forceinline__ void xyzz_add_aff(Xyzz<F> &acc, const Aff<F> &a) {
+  if (xyzz_is_inf(acc)) { xyzz_from_aff(acc, a); return; }
+  Fe<F> P, R, t;
+  fe_mul(P, a.x, acc.ZZ);      // U2 = X2*ZZ1
+  fe_sub(P, P, acc.X);         // P  = U2 - X1
+  fe_mul(R, a.y, acc.ZZZ);     // S2 = Y2*ZZZ1
+  fe_sub(R, R, acc.Y);         // R  = S2 - Y1
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) { xyzz_dbl_aff(acc, a); }
+    else { xyzz_set_inf(acc); }
+    return;
+  }
+  Fe<F> PP, PPP, Q;
+  fe_sqr(PP, P);
+  fe_mul(PPP, P, PP);
+  fe_mul(Q, acc.X, PP);
+  fe_sqr(t, R);
+  fe_sub(t, t, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(t, t, Q);             // X3 = R^2 - PPP - 2Q
+  fe_sub(Q, Q, t);
+  fe_mul(Q, R, Q);             // R*(Q - X3)
+  fe_mul(R, acc.Y, PPP);       // Y1*PPP
+  fe_sub(acc.Y, Q, R);
+  acc.X = t;
+  fe_mul(acc.ZZ, acc.ZZ, PP);
+  fe_mul(acc.ZZZ, acc.ZZZ, PPP);
+}
+
+// acc += b  (add-2008-s), all special cases handled
+template <class F>
+__device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
+  if (xyzz_is_inf(b)) return;
+  if (xyzz_is_inf(acc)) { acc = b; return; }
+  Fe<F> U1, S1, P, R, t;
+  fe_mul(U1, acc.X, b.ZZ);     // U1 = X1*ZZ2
+  fe_mul(P, b.X, acc.ZZ);      // U2 = X2*ZZ1
+  fe_sub(P, P, U1);            // P = U2 - U1
+  fe_mul(S1, acc.Y, b.ZZZ);    // S1 = Y1*ZZZ2
+  fe_mul(R, b.Y, acc.ZZZ);     // S2 = Y2*ZZZ1
+  fe_sub(R, R, S1);            // R = S2 - S1
+  if (fe_is_zero(P)) {
+    if (fe_is_zero(R)) { xyzz_dbl(acc, b); }
+    else { xyzz_set_inf(acc); }
+    return;
+  }
+  Fe<F> PP, PPP, Q;
+  fe_sqr(PP, P);
+  fe_mul(PPP, P, PP);
+  fe_mul(Q, U1, PP);
+  fe_sqr(t, R);
+  fe_sub(t, t, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(t, t, Q);             // X3
+  fe_sub(Q, Q, t);
+  fe_mul(Q, R, Q);
+  fe_mul(S1, S1, PPP);
+  fe_sub(acc.Y, Q, S1);
+  acc.X = t;
+  fe_mul(acc.ZZ, acc.ZZ, b.ZZ);
+  fe_mul(acc.ZZ, acc.ZZ, PP);
+  fe_mul(acc.ZZZ, acc.ZZZ, b.ZZZ);
+  fe_mul(acc.ZZZ, acc.ZZZ, PPP);
+}
+
+// affine point load with the 0xFF-sentinel infinity check; returns false for infinity
+template <class F>
+__device__ __forceinline__ bool aff_load(Aff<F> &a, const uint64_t *__restrict__ p) {
+  fe_load(a.x, p);
+  fe_load(a.y, p + F::N64);
+  uint32_t all = 0xffffffffu;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) all &= a.x.v[i] & a.y.v[i];
+  return all != 0xffffffffu;
+}
+
+}  // namespace zk

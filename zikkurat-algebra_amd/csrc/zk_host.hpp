@@ -1,0 +1,280 @@
+// zk_host.hpp -- host-side (CPU) Montgomery arithmetic and G1 point ops.
+//
+// Product code, NOT the oracle: the library uses it for what is cheaper on one CPU
+// core than on a GPU lane-chain -- the final Horner combine of per-window bucket
+// sums (reference: the window loop, bls12_381_G1_proj.c:577-583), the affine /
+// normalised outputs (bls12_381_G1_proj.c:79-98, 133-145), twiddle seeds and the
+// deterministic synthetic-input generator.  Same Montgomery representation as the
+// reference (64-bit limbs, R = 2^(64*n64)); canonical outputs throughout.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+#include "zk_params.inc"
+
+namespace zkh {
+
+typedef unsigned __int128 u128;
+
+#define ZKH_DEFINE_FIELD(NAME, PFX)                                                   \
+  struct NAME {                                                                       \
+    static constexpr int N = PFX##_N64;                                               \
+    static constexpr int BITS = PFX##_BITS;                                           \
+    static constexpr uint64_t MINV = PFX##_MINV64;                                    \
+    static constexpr uint64_t P[N] = PFX##_P64;                                       \
+    static constexpr uint64_t ONE[N] = PFX##_R64;                                     \
+    static constexpr uint64_t R2[N] = PFX##_R2_64;                                    \
+  };
+
+ZKH_DEFINE_FIELD(BN_Fp, ZK_BN128_FP)
+ZKH_DEFINE_FIELD(BN_Fr, ZK_BN128_FR)
+ZKH_DEFINE_FIELD(BLS_Fp, ZK_BLS12_381_FP)
+ZKH_DEFINE_FIELD(BLS_Fr, ZK_BLS12_381_FR)
+
+template <class F>
+struct Fe {
+  uint64_t v[F::N];
+};
+
+template <class F> inline void set_zero(Fe<F> &r) { memset(r.v, 0, sizeof r.v); }
+template <class F> inline void set_one(Fe<F> &r) { memcpy(r.v, F::ONE, sizeof r.v); }
+template <class F> inline bool is_zero(const Fe<F> &a) {
+  uint64_t acc = 0;
+  for (int i = 0; i < F::N; i++) acc |= a.v[i];
+  return acc == 0;
+}
+template <class F> inline bool eq(const Fe<F> &a, const Fe<F> &b) {
+  return memcmp(a.v, b.v, sizeof a.v) == 0;
+}
+template <class F> inline bool is_one(const Fe<F> &a) { return memcmp(a.v, F::ONE, sizeof a.v) == 0; }
+
+// x >= p ?
+template <class F> inline bool geq_p(const uint64_t *x) {
+  for (int i = F::N - 1; i >= 0; i--) {
+    if (x[i] != F::P[i]) return x[i] > F::P[i];
+  }
+  return true;
+}
+template <class F> inline void sub_p(uint64_t *x) {
+  uint64_t br = 0;
+  for (int i = 0; i < F::N; i++) {
+    u128 d = (u128)x[i] - F::P[i] - br;
+    x[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+}
+template <class F> inline void add(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  uint64_t c = 0;
+  for (int i = 0; i < F::N; i++) {
+    u128 s = (u128)a.v[i] + b.v[i] + c;
+    r.v[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
+  }
+  if (geq_p<F>(r.v)) sub_p<F>(r.v);  // spare top bits: no carry out
+}
+template <class F> inline void sub(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  uint64_t br = 0;
+  for (int i = 0; i < F::N; i++) {
+    u128 d = (u128)a.v[i] - b.v[i] - br;
+    r.v[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+  if (br) {
+    uint64_t c = 0;
+    for (int i = 0; i < F::N; i++) {
+      u128 s = (u128)r.v[i] + F::P[i] + c;
+      r.v[i] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+  }
+}
+template <class F> inline void neg(Fe<F> &r, const Fe<F> &a) {
+  Fe<F> z;
+  set_zero(z);
+  sub(r, z, a);
+}
+// Montgomery product (CIOS, 64-bit limbs)
+template <class F> inline void mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  constexpr int N = F::N;
+  uint64_t t[N + 2];
+  memset(t, 0, sizeof t);
+  for (int i = 0; i < N; i++) {
+    uint64_t c = 0;
+    for (int j = 0; j < N; j++) {
+      u128 x = (u128)a.v[j] * b.v[i] + t[j] + c;
+      t[j] = (uint64_t)x;
+      c = (uint64_t)(x >> 64);
+    }
+    u128 s = (u128)t[N] + c;
+    t[N] = (uint64_t)s;
+    t[N + 1] = (uint64_t)(s >> 64);
+    uint64_t m = t[0] * F::MINV;
+    u128 x = (u128)m * F::P[0] + t[0];
+    c = (uint64_t)(x >> 64);
+    for (int j = 1; j < N; j++) {
+      x = (u128)m * F::P[j] + t[j] + c;
+      t[j - 1] = (uint64_t)x;
+      c = (uint64_t)(x >> 64);
+    }
+    s = (u128)t[N] + c;
+    t[N - 1] = (uint64_t)s;
+    t[N] = t[N + 1] + (uint64_t)(s >> 64);
+  }
+  memcpy(r.v, t, sizeof r.v);
+  if (t[N] || geq_p<F>(r.v)) sub_p<F>(r.v);
+}
+template <class F> inline void sqr(Fe<F> &r, const Fe<F> &a) { mul(r, a, a); }
+
+// standard <-> Montgomery
+template <class F> inline void to_mont(Fe<F> &r, const Fe<F> &a) {
+  Fe<F> r2;
+  memcpy(r2.v, F::R2, sizeof r2.v);
+  mul(r, a, r2);
+}
+template <class F> inline void from_mont(Fe<F> &r, const Fe<F> &a) {
+  Fe<F> one;
+  set_zero(one);
+  one.v[0] = 1;
+  mul(r, a, one);
+}
+
+// a^e for a little-endian exponent of `ne` words (Montgomery in, Montgomery out)
+template <class F> inline void pow(Fe<F> &r, const Fe<F> &a, const uint64_t *e, int ne) {
+  Fe<F> acc, base = a;
+  set_one(acc);
+  for (int i = 0; i < ne; i++) {
+    uint64_t w = e[i];
+    for (int b = 0; b < 64; b++) {
+      if (w & 1) mul(acc, acc, base);
+      sqr(base, base);
+      w >>= 1;
+    }
+  }
+  r = acc;
+}
+// inverse via Fermat (a^(p-2)); 0 -> 0 like the reference (Fr_std.c:298-301)
+template <class F> inline void inv(Fe<F> &r, const Fe<F> &a) {
+  if (is_zero(a)) { set_zero(r); return; }
+  uint64_t e[F::N];
+  memcpy(e, F::P, sizeof e);
+  // p - 2 (p odd, p > 2: no borrow past limb 0 unless P[0] < 2)
+  uint64_t br = 2;
+  for (int i = 0; i < F::N && br; i++) {
+    uint64_t o = e[i];
+    e[i] = o - br;
+    br = (o < br) ? 1 : 0;
+  }
+  pow(r, a, e, F::N);
+}
+
+// ---------------------------------------------------------------------------
+// G1 in homogeneous projective coordinates (x = X/Z, y = Y/Z), a = 0.
+// Infinity: Z == 0 (canonical form (0 : 1 : 0), reference set_infinity
+// bls12_381_G1_proj.c:179-183).  Affine infinity: all-0xFF bytes (G1_affine.c:1-6).
+
+template <class F>
+struct Proj {
+  Fe<F> X, Y, Z;
+};
+template <class F>
+struct Aff {
+  Fe<F> x, y;
+};
+
+template <class F> inline void proj_set_inf(Proj<F> &r) {
+  set_zero(r.X);
+  set_one(r.Y);
+  set_zero(r.Z);
+}
+template <class F> inline bool proj_is_inf(const Proj<F> &a) { return is_zero(a.Z); }
+template <class F> inline bool aff_is_inf(const Aff<F> &a) {
+  for (int i = 0; i < F::N; i++)
+    if (a.x.v[i] != ~0ull || a.y.v[i] != ~0ull) return false;
+  return true;
+}
+template <class F> inline void aff_set_inf(Aff<F> &a) { memset(&a, 0xff, sizeof a); }
+
+template <class F> inline void proj_from_aff(Proj<F> &r, const Aff<F> &a) {
+  if (aff_is_inf(a)) { proj_set_inf(r); return; }
+  r.X = a.x;
+  r.Y = a.y;
+  set_one(r.Z);
+}
+
+// complete addition for a = 0 (Renes-Costello-Batina 2015, alg. 7); b3 = 3*B (Montgomery)
+template <class F> inline void proj_add(Proj<F> &r, const Proj<F> &P, const Proj<F> &Q, const Fe<F> &b3) {
+  Fe<F> t0, t1, t2, t3, t4, X3, Y3, Z3;
+  mul(t0, P.X, Q.X);
+  mul(t1, P.Y, Q.Y);
+  mul(t2, P.Z, Q.Z);
+  add(t3, P.X, P.Y);
+  add(t4, Q.X, Q.Y);
+  mul(t3, t3, t4);
+  add(t4, t0, t1);
+  sub(t3, t3, t4);
+  add(t4, P.Y, P.Z);
+  add(X3, Q.Y, Q.Z);
+  mul(t4, t4, X3);
+  add(X3, t1, t2);
+  sub(t4, t4, X3);
+  add(X3, P.X, P.Z);
+  add(Y3, Q.X, Q.Z);
+  mul(X3, X3, Y3);
+  add(Y3, t0, t2);
+  sub(Y3, X3, Y3);
+  add(X3, t0, t0);
+  add(t0, X3, t0);
+  mul(t2, b3, t2);
+  add(Z3, t1, t2);
+  sub(t1, t1, t2);
+  mul(Y3, b3, Y3);
+  mul(X3, t4, Y3);
+  mul(t2, t3, t1);
+  sub(X3, t2, X3);
+  mul(Y3, Y3, t0);
+  mul(t1, t1, Z3);
+  add(Y3, t1, Y3);
+  mul(t0, t0, t3);
+  mul(Z3, Z3, t4);
+  add(Z3, Z3, t0);
+  r.X = X3;
+  r.Y = Y3;
+  r.Z = Z3;
+}
+template <class F> inline void proj_dbl(Proj<F> &r, const Proj<F> &P, const Fe<F> &b3) {
+  proj_add(r, P, P, b3);  // the complete formula doubles correctly
+}
+
+template <class F> inline void proj_to_aff(Aff<F> &r, const Proj<F> &P) {
+  if (is_zero(P.Z)) { aff_set_inf(r); return; }
+  Fe<F> zi;
+  inv(zi, P.Z);
+  mul(r.x, P.X, zi);
+  mul(r.y, P.Y, zi);
+}
+// canonical projective form: Z = 1, or (0 : 1 : 0) for infinity (reference normalize,
+// bls12_381_G1_proj.c:79-98)
+template <class F> inline void proj_normalize(Proj<F> &r, const Proj<F> &P) {
+  if (is_zero(P.Z)) { proj_set_inf(r); return; }
+  if (is_one(P.Z)) { r = P; return; }
+  Fe<F> zi;
+  inv(zi, P.Z);
+  mul(r.X, P.X, zi);
+  mul(r.Y, P.Y, zi);
+  set_one(r.Z);
+}
+
+// k * P for a little-endian multi-word integer k (double-and-add, MSB first)
+template <class F> inline void proj_scale(Proj<F> &r, const Proj<F> &P, const uint64_t *k, int nk,
+                                          const Fe<F> &b3) {
+  Proj<F> acc;
+  proj_set_inf(acc);
+  for (int i = nk - 1; i >= 0; i--) {
+    for (int b = 63; b >= 0; b--) {
+      proj_dbl(acc, acc, b3);
+      if ((k[i] >> b) & 1) proj_add(acc, acc, P, b3);
+    }
+  }
+  r = acc;
+}
+
+}  // namespace zkh

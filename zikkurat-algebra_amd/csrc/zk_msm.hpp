@@ -1,0 +1,31 @@
+// zk_msm.hpp -- C++ interface of the device MSM (used by the C ABI layer)
+#pragma once
+#include <stdint.h>
+#include "zk_curve.hpp"
+#include "zk_host.hpp"
+
+namespace zk {
+
+template <class C> struct HostOf;
+template <> struct HostOf<BN254> {
+  using Fp = zkh::BN_Fp;
+  using Fr = zkh::BN_Fr;
+  static void b3(zkh::Fe<Fp> &r) { const uint64_t v[] = ZK_BN128_B3_FP64; memcpy(r.v, v, sizeof r.v); }
+};
+template <> struct HostOf<BLS381> {
+  using Fp = zkh::BLS_Fp;
+  using Fr = zkh::BLS_Fr;
+  static void b3(zkh::Fe<Fp> &r) { const uint64_t v[] = ZK_BLS12_381_B3_FP64; memcpy(r.v, v, sizeof r.v); }
+};
+
+int msm_default_window(int n);
+
+// scalars: n x nl u64 (nl in 1..4) (Montgomery Fr if mont, else plain 256-bit integers)
+// points : n x 2*NP64 u64 affine Montgomery (all-0xFF = infinity)
+// out    : 3*NP64 u64 projective, reference Montgomery form, NOT normalised
+// host_inputs: pointers are host memory (staged by the call) vs device-resident
+template <class C>
+void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs, bool mont,
+            int window, uint64_t *out_proj);
+
+}  // namespace zk

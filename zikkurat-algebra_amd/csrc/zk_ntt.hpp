@@ -1,0 +1,10 @@
+// zk_ntt.hpp -- C++ interface of the device NTT (used by the C ABI layer)
+#pragma once
+#include <stdint.h>
+namespace zk {
+// curve: 0 = bn128, 1 = bls12_381.  gen_mont: generator of the order-2^m subgroup
+// (Montgomery Fr, HOST pointer).  src/dst: 2^m x 4 u64 Montgomery Fr; host pointers
+// when host_io, device pointers otherwise.  inverse: interpolation incl. the 1/N factor.
+void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst, bool host_io,
+         bool inverse);
+}  // namespace zk

@@ -1,0 +1,93 @@
+"""GPU MSM parity through the C ABI: bit-exact against the reference-generated golden
+vectors, the oracle, and (at BASELINE sizes) the reference's own outputs."""
+import numpy as np
+import pytest
+
+from golden_io import baseline_configs, msm_cases
+
+pytestmark = pytest.mark.gpu
+CURVES = ["bn128", "bls12_381"]
+FR_FLD = {"bn128": 1, "bls12_381": 3}
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_golden_affine_and_projective(gpu, curve):
+    for name, sc, pts, mont, aff, projn in msm_cases(curve):
+        got = gpu.msm_affine(curve, sc, pts, std=not mont)
+        assert np.array_equal(got, aff), name
+        proj = gpu.msm(curve, sc, pts) if mont else gpu.msm_std(curve, sc, pts)
+        assert np.array_equal(proj, projn), name
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_golden_jacobian(gpu, oracle, curve):
+    NP = gpu.NLIMBS_P[curve]
+    for name, sc, pts, mont, aff, projn in msm_cases(curve):
+        jac = gpu.msm_jac(curve, sc, pts, std=not mont)
+        if np.all(aff == np.uint64(0xFFFFFFFFFFFFFFFF)):
+            assert not jac[2 * NP:].any() and jac[:NP].any(), name   # (1:1:0)
+        else:
+            assert np.array_equal(jac[:2 * NP], aff), name          # Z = 1 => (x, y)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("window", [4, 5, 9, 13, 16, 20])
+def test_window_independence(gpu, oracle, curve, window):
+    sc = oracle.to_std(FR_FLD[curve], gpu.gen_fr(curve, 31, 3000))
+    pts = gpu.gen_points(curve, 32, 3000)
+    want = oracle.normalize(curve, oracle.msm(curve, sc, pts, mont=False, out="proj"))
+    assert np.array_equal(gpu.msm_variable(curve, sc, pts, window), want)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("n", [0, 1, 2, 7, 255, 4097, 65536])
+def test_random_sizes_vs_oracle(gpu, oracle, curve, n):
+    sc = gpu.gen_fr(curve, 1000 + n, n)
+    pts = gpu.gen_points(curve, 2000 + n, n)
+    assert np.array_equal(gpu.msm_affine(curve, sc, pts), oracle.msm(curve, sc, pts, mont=True))
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_skewed_buckets(gpu, oracle, curve):
+    # every scalar equal -> one bucket per window holds all points (chunk stitching)
+    n = 20000
+    sc = np.tile(gpu.gen_fr(curve, 5, 1), (n, 1))
+    pts = gpu.gen_points(curve, 6, n)
+    assert np.array_equal(gpu.msm_affine(curve, sc, pts), oracle.msm(curve, sc, pts, mont=True))
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_device_resident_api(gpu, curve):
+    n = 5000
+    sc = gpu.gen_fr(curve, 41, n)
+    pts = gpu.gen_points(curve, 42, n)
+    ds, dp = gpu.DeviceBuffer(sc), gpu.DeviceBuffer(pts)
+    try:
+        assert np.array_equal(gpu.msm_device(curve, n, ds, dp), gpu.msm(curve, sc, pts))
+    finally:
+        ds.free(); dp.free()
+
+
+def _baseline(key):
+    cfg = baseline_configs().get(key)
+    if cfg is None:
+        pytest.skip(f"{key} not in tests/golden/baseline_configs.json")
+    return cfg
+
+
+def test_config2_bls12_381_msm_2_20_vs_reference(gpu):
+    cfg = _baseline("config2_bls12_381_msm_2^20")
+    n = 1 << cfg["log_n"]
+    sc = gpu.gen_fr("bls12_381", cfg["seed"], n)
+    pts = gpu.gen_points("bls12_381", cfg["seed"], n)
+    got = gpu.msm_affine("bls12_381", sc, pts)
+    assert [int(x) for x in got] == cfg["affine"]
+
+
+def test_config4_bn128_msm_2_24_vs_reference(gpu):
+    cfg = _baseline("config4_bn128_msm_2^24")
+    n = 1 << cfg["log_n"]
+    sc = gpu.gen_fr("bn128", cfg["seed"], n)
+    pts = gpu.gen_points("bn128", cfg["seed"], n)
+    got = gpu.msm_affine("bn128", sc, pts)
+    assert [int(x) for x in got] == cfg["affine"]

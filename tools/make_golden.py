@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Generate the golden parity fixtures under tests/golden/ FROM THE REFERENCE ITSELF.
+
+The reference ships no golden vectors for MSM/NTT (its tests are
+unseeded random properties), so the expected outputs here are produced by running the
+reference's own generated C (oracle/_ref/libzkref.so, built in place from
+/root/reference/lib/cbits by oracle/Makefile) on deterministic inputs.  Inputs come from
+the documented synthetic-input generator (zikkurat-algebra_amd/csrc/zk_gen.cpp; an
+independent restatement in oracle/zk_oracle.c is checked equal by the tests).
+
+  python tools/make_golden.py small   # edge-case MSM + NTT vectors (stored in full)  ~1 min
+  python tools/make_golden.py large   # BASELINE-config outputs / SHA-256 digests     ~10 min, 8 cores
+
+Only this script (in this container, where /root/reference exists) runs the reference;
+the GPU box only reads the committed .npz/.json files.
+"""
+import hashlib
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+from oracle.oracle import Reference, Oracle  # noqa: E402
+import zkalgebra as zk  # noqa: E402  (host-only functions: generator, fft generator)
+
+R_ORDER = {
+    "bn128": 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001,
+    "bls12_381": 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001,
+}
+FLD_FR = {"bn128": 1, "bls12_381": 3}
+
+
+def limbs(x, n=4):
+    return np.array([(x >> (64 * i)) & ((1 << 64) - 1) for i in range(n)], dtype=np.uint64)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# ----------------------------------------------------------------------------- small fixtures
+
+def msm_cases(curve):
+    """Edge cases the reference's semantics define."""
+    o = Oracle()
+    NP = zk.NLIMBS_P[curve]
+    r = R_ORDER[curve]
+    cases = []
+    for n in (1, 2, 3, 17, 64, 1000, 4096):
+        cases.append((f"random_n{n}", zk.gen_fr(curve, 100 + n, n), zk.gen_points(curve, 200 + n, n), True))
+    # std-coefficient variants of the same data (to_std of the Montgomery scalars)
+    for n in (17, 1000):
+        sc = zk.gen_fr(curve, 100 + n, n)
+        cases.append((f"std_n{n}", o.to_std(FLD_FR[curve], sc.copy()), zk.gen_points(curve, 200 + n, n), False))
+    n = 64
+    pts = zk.gen_points(curve, 7, n)
+    sc = zk.gen_fr(curve, 8, n)
+    z = sc.copy(); z[::3] = 0
+    cases.append(("zero_scalars", z, pts, True))
+    cases.append(("all_zero", np.zeros_like(sc), pts, True))
+    top = np.tile(limbs(r - 1), (n, 1))
+    cases.append(("std_r_minus_1", top.copy(), pts, False))
+    full = np.full((n, 4), np.uint64(0xFFFFFFFFFFFFFFFF))
+    cases.append(("std_2pow256_minus_1", full, pts, False))
+    eq = np.tile(sc[0], (n, 1))
+    cases.append(("all_equal_scalars", eq, pts, True))
+    dup = np.tile(pts[0], (n, 1))
+    cases.append(("duplicate_points", sc.copy(), dup, True))
+    # P and -P with equal scalars -> cancels (negate y: p - y)
+    neg = pts.copy()
+    pfield = {"bn128": 0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47,
+              "bls12_381": 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB}[curve]
+    for i in range(n):
+        y = sum(int(neg[i, NP + j]) << (64 * j) for j in range(NP))
+        neg[i, NP:] = limbs((pfield - y) % pfield, NP)
+    pm = np.concatenate([pts[:32], neg[:32]])
+    cs = np.concatenate([sc[:32], sc[:32]])
+    cases.append(("p_and_minus_p", cs, pm, True))
+    infp = pts.copy(); infp[5:40:4] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    cases.append(("infinity_points", sc.copy(), infp, True))
+    allinf = np.full_like(pts, np.uint64(0xFFFFFFFFFFFFFFFF))
+    cases.append(("all_infinity", sc.copy(), allinf, True))
+    small = np.zeros_like(sc); small[:, 0] = np.arange(1, n + 1, dtype=np.uint64)
+    cases.append(("std_small_scalars", small, pts, False))
+    one_limb = zk.gen_fr(curve, 9, 200)[:, :1].copy()
+    cases.append(("std_one_limb", one_limb, zk.gen_points(curve, 10, 200), False))
+    return cases
+
+
+def make_small():
+    os.makedirs(GOLD, exist_ok=True)
+    ref = Reference()
+    for curve in zk.CURVES:
+        arrays = {}
+        names = []
+        t = time.time()
+        for name, sc, pts, mont in msm_cases(curve):
+            sc = np.ascontiguousarray(sc, dtype=np.uint64)
+            pts = np.ascontiguousarray(pts, dtype=np.uint64)
+            aff = ref.msm(curve, sc, pts, mont=mont, out="affine")
+            proj = ref.msm(curve, sc, pts, mont=mont, out="proj")
+            names.append(name)
+            arrays[f"{name}__scalars"] = sc
+            arrays[f"{name}__points"] = pts
+            arrays[f"{name}__mont"] = np.array([1 if mont else 0], dtype=np.uint64)
+            arrays[f"{name}__affine"] = aff
+            arrays[f"{name}__proj_normalized"] = ref.normalize(curve, proj)
+        np.savez_compressed(os.path.join(GOLD, f"msm_{curve}.npz"), names=np.array(names), **arrays)
+        print(curve, "msm fixtures", len(names), "%.1fs" % (time.time() - t))
+        # NTT
+        arrays = {}
+        for m in (0, 1, 2, 3, 5, 8, 10, 12):
+            g = zk.get_fft_subgroup(curve, m).gen_array()
+            x = zk.gen_fr(curve, 300 + m, 1 << m)
+            f = ref.ntt(curve, m, g, x)
+            i = ref.ntt(curve, m, g, x, inverse=True)
+            arrays[f"m{m}__input"] = x
+            arrays[f"m{m}__gen"] = g
+            arrays[f"m{m}__forward"] = f
+            arrays[f"m{m}__inverse"] = i
+        np.savez_compressed(os.path.join(GOLD, f"ntt_{curve}.npz"), **arrays)
+        print(curve, "ntt fixtures")
+
+
+# ----------------------------------------------------------------------------- large (BASELINE configs)
+
+def _shard_msm(args):
+    curve, seed, lo, hi, mont = args
+    sc = zk.gen_fr(curve, seed, hi - lo, start=lo)
+    if not mont:
+        sc = Oracle().to_std(FLD_FR[curve], sc)
+    pts = zk.gen_points(curve, seed, hi - lo, start=lo)
+    ref = Reference()
+    t = time.time()
+    p = ref.msm(curve, sc, pts, mont=mont, out="proj")
+    return p, time.time() - t
+
+
+def large_msm(curve, logn, seed, shards):
+    n = 1 << logn
+    step = n // shards
+    # the reference's Montgomery entry aborts at 2^26 (int overflow, G1_proj.c:631-632): use the
+    # std entry on to_std'd scalars there -- same mathematical input.
+    mont = logn < 26
+    with mp.Pool(min(shards, 8)) as pool:
+        parts = pool.map(_shard_msm, [(curve, seed, k * step, (k + 1) * step, mont) for k in range(shards)])
+    ref = Reference()
+    acc = parts[0][0]
+    for p, _ in parts[1:]:
+        acc = ref.proj_add(curve, acc, p)
+    aff = ref.to_affine(curve, acc)
+    cpu_s = sum(t for _, t in parts)
+    return {"curve": curve, "log_n": logn, "seed": seed, "affine": [int(x) for x in aff],
+            "reference_cpu_seconds_sum_over_shards": cpu_s, "shards": shards,
+            "reference_entry": "MSM_mont_coeff_proj_out" if mont else "MSM_std_coeff_proj_out (to_std scalars)"}
+
+
+def large_ntt(curve, logn, seed):
+    ref = Reference()
+    g = zk.get_fft_subgroup(curve, logn).gen_array()
+    x = zk.gen_fr(curve, seed, 1 << logn)
+    t = time.time()
+    f = ref.ntt(curve, logn, g, x)
+    tf = time.time() - t
+    t = time.time()
+    i = ref.ntt(curve, logn, g, f, inverse=True)
+    ti = time.time() - t
+    assert np.array_equal(i, x), "reference NTT round trip failed"
+    return {"curve": curve, "log_n": logn, "seed": seed, "input_sha256": sha(x), "forward_sha256": sha(f),
+            "forward_first": [int(v) for v in f[0]], "forward_last": [int(v) for v in f[-1]],
+            "roundtrip_ok": True, "reference_forward_seconds": tf, "reference_inverse_seconds": ti}
+
+
+def make_large(which):
+    os.makedirs(GOLD, exist_ok=True)
+    path = os.path.join(GOLD, "baseline_configs.json")
+    data = json.load(open(path)) if os.path.exists(path) else {}
+    jobs = {
+        "config1_bn128_ntt_2^14": lambda: large_ntt("bn128", 14, 0x5A4B0001),
+        "config2_bls12_381_msm_2^20": lambda: large_msm("bls12_381", 20, 0x5A4B0002, 8),
+        "config3_bls12_381_ntt_2^24": lambda: large_ntt("bls12_381", 24, 0x5A4B0003),
+        "config4_bn128_msm_2^24": lambda: large_msm("bn128", 24, 0x5A4B0004, 8),
+        "config5_bls12_381_msm_2^26": lambda: large_msm("bls12_381", 26, 0x5A4B0005, 8),
+    }
+    for k, fn in jobs.items():
+        if which and which not in k:
+            continue
+        t = time.time()
+        data[k] = fn()
+        data[k]["wall_seconds"] = time.time() - t
+        print(k, "done in %.1fs" % (time.time() - t), flush=True)
+        json.dump(data, open(path, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    if len(sys.argv) < 2 or sys.argv[1] not in ("small", "large"):
+        print(__doc__)
+        sys.exit(2)
+    if sys.argv[1] == "small":
+        make_small()
+    else:
+        make_large(sys.argv[2] if len(sys.argv) > 2 else None)

@@ -1,0 +1,295 @@
+"""Host-side mirror of the reference's MSM / NTT API, over the gfx950 C-ABI library.
+
+The reference exposes this path to users through Haskell:
+
+    ZK.Algebra.Curves.<C>.G1.Proj.msm      :: FlatArray Fr -> FlatArray Affine.G1 -> G1   (G1/Proj.hs:237-246)
+    ZK.Algebra.Curves.<C>.G1.Proj.msmStd   :: FlatArray Std.Fr -> FlatArray Affine.G1 -> G1 (G1/Proj.hs:253-262)
+    ZK.Algebra.Curves.<C>.G1.Proj.msmProj  :: FlatArray Fr -> FlatArray G1 -> G1         (G1/Proj.hs:222-223)
+    ZK.Algebra.Curves.<C>.G1.Affine.msm    = toAffine . Proj.msm                           (G1/Affine.hs:143-149)
+    ZK.Algebra.Curves.<C>.Poly.forwardNTT  :: FFTSubgroup Fr -> Poly -> FlatArray Fr       (Poly.hs:400-410)
+    ZK.Algebra.Curves.<C>.Poly.inverseNTT  :: FFTSubgroup Fr -> FlatArray Fr -> Poly       (Poly.hs:412-422)
+    ZK.Algebra.Class.FFT.getFFTSubgroup    :: Log2 -> FFTSubgroup                          (Class/FFT.hs:60-66)
+
+GHC is not available in this image, so this module is the host-language mirror
+(same names in snake_case, same argument meaning, same error messages) used by the
+tests and the benchmark.  ``FlatArray`` is a C-contiguous ``numpy.uint64`` array of
+shape (n, limbs) -- byte-identical to the reference's pinned FlatArray memory
+(Class/Flat.hs:81-83).  Every call goes through the C ABI of
+``lib/libzkalgebra_gpu.so`` and runs on the GPU; if the library or a GPU is missing,
+calls raise -- there is no CPU fallback.
+"""
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libzkalgebra_gpu.so")
+U64P = ctypes.POINTER(ctypes.c_uint64)
+
+CURVES = ("bn128", "bls12_381")
+CURVE_ID = {"bn128": 0, "bls12_381": 1}
+NLIMBS_P = {"bn128": 4, "bls12_381": 6}   # base field limbs (NLIMBS_P in G1_proj.c:17)
+NLIMBS_R = 4                               # scalar field limbs
+FFT_LOG = {"bn128": 28, "bls12_381": 32}   # 2-adicity of the FFT domain (Fr/Mont.hs fftDomain)
+
+# every exported symbol of include/zkalgebra_gpu.h (checked by tests/test_capi.py)
+REFERENCE_SYMBOLS = [
+    f"{c}_G1_proj_MSM_{k}_coeff_{o}_out" for c in CURVES for k in ("mont", "std") for o in ("proj", "affine")
+] + [f"{c}_G1_proj_MSM_std_coeff_proj_out_variable" for c in CURVES] + [
+    f"{c}_G1_jac_MSM_{k}_coeff_{o}_out" for c in CURVES for k in ("mont", "std") for o in ("jac", "affine")
+] + [f"{c}_poly_mont_ntt_{d}" for c in CURVES for d in ("forward", "inverse")]
+EXTENSION_SYMBOLS = [
+    "zkg_version", "zkg_device_count", "zkg_set_device", "zkg_device_malloc", "zkg_device_free",
+    "zkg_memcpy_htod", "zkg_memcpy_dtoh", "zkg_device_synchronize", "zkg_g1_msm_device", "zkg_ntt_device",
+    "zkg_g1_proj_add", "zkg_g1_proj_normalize", "zkg_g1_proj_to_affine", "zkg_gen_fr", "zkg_gen_g1_points",
+    "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
+]
+
+_lib = None
+
+
+def load():
+    """Load the C-ABI library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"zkalgebra_gpu library not built: {LIB_PATH} (run __graft_entry__.build())")
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.zkg_version.restype = ctypes.c_char_p
+        lib.zkg_device_malloc.restype = ctypes.c_void_p
+        lib.zkg_device_malloc.argtypes = [ctypes.c_size_t]
+        lib.zkg_device_free.argtypes = [ctypes.c_void_p]
+        lib.zkg_memcpy_htod.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        lib.zkg_memcpy_dtoh.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        lib.zkg_g1_msm_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, U64P, ctypes.c_int]
+        lib.zkg_ntt_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, U64P, ctypes.c_void_p,
+                                       ctypes.c_void_p]
+        lib.zkg_gen_fr.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, U64P]
+        lib.zkg_gen_g1_points.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, U64P]
+        lib.zkg_timer_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    if a.dtype != np.uint64 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError("FlatArray buffers must be C-contiguous numpy.uint64 arrays")
+    return a.ctypes.data_as(U64P)
+
+
+def device_count():
+    return load().zkg_device_count()
+
+
+def require_gpu():
+    if device_count() < 1:
+        raise RuntimeError("zkalgebra_gpu: no GPU visible -- the MSM/NTT path is GPU-only (no CPU fallback)")
+
+
+# ----------------------------------------------------------------------------- FFT subgroups
+
+@dataclass(frozen=True)
+class FFTSubgroup:
+    """Mirror of ZK.Algebra.Class.FFT.FFTSubgroup (Class/FFT.hs:26-30): generator (Montgomery
+    Fr, 4 limbs) of the multiplicative subgroup of order 2^log_size."""
+    curve: str
+    gen: tuple
+    log_size: int
+
+    @property
+    def size(self):
+        return 1 << self.log_size
+
+    def gen_array(self):
+        return np.array(self.gen, dtype=np.uint64)
+
+
+def get_fft_subgroup(curve, log_size):
+    """getFFTSubgroup (Class/FFT.hs:60-66): gen_m = fftDomain^(2^(M - m))."""
+    if not (0 <= log_size <= FFT_LOG[curve]):
+        raise ValueError("getFFTSubgroup: subgroup size is too large for this field")
+    out = np.zeros(4, dtype=np.uint64)
+    load().zkg_fft_generator(CURVE_ID[curve], log_size, _p(out))
+    return FFTSubgroup(curve, tuple(int(x) for x in out), log_size)
+
+
+# ----------------------------------------------------------------------------- MSM
+
+def _check_msm(curve, coeffs, points):
+    if coeffs.ndim != 2 or points.ndim != 2 or coeffs.shape[0] != points.shape[0]:
+        raise ValueError("msm: incompatible array dimensions")   # G1/Proj.hs:239
+    if points.shape[1] != 2 * NLIMBS_P[curve]:
+        raise ValueError("msm: points must be affine (x, y) in Montgomery form")
+
+
+def msm(curve, coeffs, points):
+    """Proj.msm: Montgomery-form Fr coefficients x affine points -> projective G1 (normalised)."""
+    _check_msm(curve, coeffs, points)
+    require_gpu()
+    out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
+    getattr(load(), f"{curve}_G1_proj_MSM_mont_coeff_proj_out")(
+        coeffs.shape[0], _p(coeffs), _p(points), _p(out), coeffs.shape[1])
+    return out
+
+
+def msm_std(curve, coeffs, points):
+    """Proj.msmStd: standard-form (plain integer) coefficients, used verbatim."""
+    _check_msm(curve, coeffs, points)
+    require_gpu()
+    out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
+    getattr(load(), f"{curve}_G1_proj_MSM_std_coeff_proj_out")(
+        coeffs.shape[0], _p(coeffs), _p(points), _p(out), coeffs.shape[1])
+    return out
+
+
+def msm_affine(curve, coeffs, points, std=False):
+    """Affine.msm = toAffine . Proj.msm (G1/Affine.hs:143-149); infinity = all-0xFF."""
+    _check_msm(curve, coeffs, points)
+    require_gpu()
+    out = np.zeros(2 * NLIMBS_P[curve], dtype=np.uint64)
+    name = f"{curve}_G1_proj_MSM_{'std' if std else 'mont'}_coeff_affine_out"
+    getattr(load(), name)(coeffs.shape[0], _p(coeffs), _p(points), _p(out), coeffs.shape[1])
+    return out
+
+
+def msm_variable(curve, coeffs, points, window_size):
+    """<C>_G1_proj_MSM_std_coeff_proj_out_variable (exported, unbound by Haskell)."""
+    _check_msm(curve, coeffs, points)
+    require_gpu()
+    out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
+    getattr(load(), f"{curve}_G1_proj_MSM_std_coeff_proj_out_variable")(
+        coeffs.shape[0], _p(coeffs), _p(points), _p(out), coeffs.shape[1], int(window_size))
+    return out
+
+
+def msm_jac(curve, coeffs, points, std=False):
+    """Jac.msm (G1/Jac.hs:225-259): Jacobian output, normalised; infinity = (1:1:0)."""
+    _check_msm(curve, coeffs, points)
+    require_gpu()
+    out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
+    name = f"{curve}_G1_jac_MSM_{'std' if std else 'mont'}_coeff_jac_out"
+    getattr(load(), name)(coeffs.shape[0], _p(coeffs), _p(points), _p(out), coeffs.shape[1])
+    return out
+
+
+def msm_proj(curve, coeffs, proj_points):
+    """Proj.msmProj cs gs = msm cs (batchToAffine gs) (G1/Proj.hs:222-223)."""
+    if proj_points.ndim != 2 or proj_points.shape[1] != 3 * NLIMBS_P[curve]:
+        raise ValueError("msm: incompatible array dimensions")
+    aff = np.stack([g1_to_affine(curve, p) for p in proj_points]) if len(proj_points) else \
+        np.zeros((0, 2 * NLIMBS_P[curve]), dtype=np.uint64)
+    return msm(curve, coeffs, np.ascontiguousarray(aff))
+
+
+def g1_to_affine(curve, proj):
+    out = np.zeros(2 * NLIMBS_P[curve], dtype=np.uint64)
+    load().zkg_g1_proj_to_affine(CURVE_ID[curve], _p(np.ascontiguousarray(proj)), _p(out))
+    return out
+
+
+def g1_normalize(curve, proj):
+    out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
+    load().zkg_g1_proj_normalize(CURVE_ID[curve], _p(np.ascontiguousarray(proj)), _p(out))
+    return out
+
+
+def g1_add(curve, a, b):
+    out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
+    load().zkg_g1_proj_add(CURVE_ID[curve], _p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(b)), _p(out))
+    return out
+
+
+# ----------------------------------------------------------------------------- NTT
+
+def forward_ntt(sg, poly):
+    """Poly.forwardNTT: evaluations f(gen^k), k = 0..n-1 (Poly.hs:400-410)."""
+    if poly.ndim != 2 or sg.size != poly.shape[0]:
+        raise ValueError("forwardNTT: subgroup size differs from the array size")   # Poly.hs:403
+    require_gpu()
+    out = np.zeros_like(poly)
+    getattr(load(), f"{sg.curve}_poly_mont_ntt_forward")(sg.log_size, _p(sg.gen_array()), _p(poly), _p(out))
+    return out
+
+
+def inverse_ntt(sg, values):
+    """Poly.inverseNTT: interpolation (Poly.hs:412-422)."""
+    if values.ndim != 2 or sg.size != values.shape[0]:
+        raise ValueError("inverseNTT: subgroup size differs from the array size")   # Poly.hs:415
+    require_gpu()
+    out = np.zeros_like(values)
+    getattr(load(), f"{sg.curve}_poly_mont_ntt_inverse")(sg.log_size, _p(sg.gen_array()), _p(values), _p(out))
+    return out
+
+
+# UnivariateFFT instance (Poly.hs:424-426)
+ntt = forward_ntt
+intt = inverse_ntt
+
+
+# ----------------------------------------------------------------------------- synthetic inputs
+
+def gen_fr(curve, seed, count, start=0):
+    out = np.zeros((count, 4), dtype=np.uint64)
+    load().zkg_gen_fr(CURVE_ID[curve], seed, start, count, _p(out))
+    return out
+
+
+def gen_points(curve, seed, count, start=0):
+    out = np.zeros((count, 2 * NLIMBS_P[curve]), dtype=np.uint64)
+    load().zkg_gen_g1_points(CURVE_ID[curve], seed, start, count, _p(out))
+    return out
+
+
+# ----------------------------------------------------------------------------- device-resident helpers
+
+class DeviceBuffer:
+    """HBM buffer owned by the library's allocator (used by bench.py and the multi-GPU path)."""
+
+    def __init__(self, host_array):
+        self.nbytes = host_array.nbytes
+        self.ptr = load().zkg_device_malloc(max(1, self.nbytes))
+        load().zkg_memcpy_htod(self.ptr, host_array.ctypes.data, self.nbytes)
+
+    @classmethod
+    def empty(cls, nbytes):
+        self = cls.__new__(cls)
+        self.nbytes = nbytes
+        self.ptr = load().zkg_device_malloc(max(1, nbytes))
+        return self
+
+    def to_host(self, like):
+        out = np.empty_like(like)
+        load().zkg_memcpy_dtoh(out.ctypes.data, self.ptr, self.nbytes)
+        return out
+
+    def free(self):
+        if self.ptr:
+            load().zkg_device_free(self.ptr)
+            self.ptr = None
+
+
+def msm_device(curve, n, d_scalars, d_points, mont=True, window=0):
+    out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
+    load().zkg_g1_msm_device(CURVE_ID[curve], n, d_scalars.ptr, 4, 1 if mont else 0, d_points.ptr, _p(out),
+                             window)
+    return out
+
+
+def ntt_device(curve, m, gen, d_src, d_dst, inverse=False):
+    load().zkg_ntt_device(CURVE_ID[curve], 1 if inverse else 0, m, _p(np.ascontiguousarray(gen)), d_src.ptr,
+                          d_dst.ptr)
+
+
+def timer(enable=None, reset=False):
+    lib = load()
+    if enable is not None:
+        lib.zkg_timer_enable(1 if enable else 0)
+    if reset:
+        lib.zkg_timer_reset()
+    ms = ctypes.c_double()
+    n = ctypes.c_long()
+    lib.zkg_timer_read(ctypes.byref(ms), ctypes.byref(n))
+    return ms.value, n.value

@@ -70,16 +70,16 @@ template <class F>
 __global__ void k_fmul(const uint64_t *in, uint64_t *out) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   Fe<F> x[2], y;
-  fe_load(x[0], in + (size_t)((t) & 1023) * F::N64);
-  fe_load(x[1], in + (size_t)((t + 1) & 1023) * F::N64);
-  fe_load(y, in + (size_t)((t + 5) & 1023) * F::N64);
+  fe_load_ref(x[0], in + (size_t)((t) & 1023) * F::N64);
+  fe_load_ref(x[1], in + (size_t)((t + 1) & 1023) * F::N64);
+  fe_load_ref(y, in + (size_t)((t + 5) & 1023) * F::N64);
   for (int i = 0; i < ITERS / 4; i++) {
     fe_mul(x[0], x[0], y);
     fe_mul(x[1], x[1], y);
   }
   Fe<F> z;
   fe_add(z, x[0], x[1]);
-  fe_store(out + (size_t)t * F::N64, z);
+  fe_store_ref(out + (size_t)t * F::N64, z);
 }
 
 // ---- prototype: unsaturated radix-2^28 Montgomery product for the 381-bit field (14 limbs)

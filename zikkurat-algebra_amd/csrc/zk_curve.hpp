@@ -168,15 +168,41 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
   fe_mul(acc.ZZZ, acc.ZZZ, PPP);
 }
 
-// affine point load with the 0xFF-sentinel infinity check; returns false for infinity
+// Affine points on the device are kept in INTERNAL form (converted once per call by
+// k_points_int): 2 x SN u32 words; the reference's all-0xFF infinity sentinel becomes a
+// first word of 0xFFFFFFFF (never a valid limb).  Returns false for infinity.
 template <class F>
-__device__ __forceinline__ bool aff_load(Aff<F> &a, const uint64_t *__restrict__ p) {
-  fe_load(a.x, p);
-  fe_load(a.y, p + F::N64);
+__device__ __forceinline__ bool aff_load(Aff<F> &a, const uint32_t *__restrict__ p) {
+  fe_load_u(a.x, p);
+  fe_load_u(a.y, p + F::SN);
+  return a.x.v[0] != 0xffffffffu;
+}
+
+// reference-form affine point (x || y, N64 u64 each) -> internal-form storage
+template <class F>
+__device__ __forceinline__ void aff_ref_to_int(uint32_t *__restrict__ out, const uint64_t *__restrict__ in) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(in);
   uint32_t all = 0xffffffffu;
+  uint32_t w[2 * F::NW];
 #pragma unroll
-  for (int i = 0; i < F::N; i++) all &= a.x.v[i] & a.y.v[i];
-  return all != 0xffffffffu;
+  for (int i = 0; i < F::NW / 2; i++) {
+    uint4 x = q[i];
+    w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
+    all &= x.x & x.y & x.z & x.w;
+  }
+  if (all == 0xffffffffu) {
+    uint4 *o = reinterpret_cast<uint4 *>(out);
+#pragma unroll
+    for (int i = 0; i < F::SN / 2; i++) o[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    return;
+  }
+  Fe<F> x, y, t;
+  fe_unpack(t, w);
+  fe_to_int(x, t);
+  fe_unpack(t, w + F::NW);
+  fe_to_int(y, t);
+  fe_store_u(out, x);
+  fe_store_u(out + F::SN, y);
 }
 
 }  // namespace zk

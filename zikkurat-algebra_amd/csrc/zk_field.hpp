@@ -1,20 +1,27 @@
-// zk_field.hpp -- prime-field arithmetic in Montgomery form for gfx950 (device)
+// zk_field.hpp -- prime-field arithmetic for gfx950 (device), unsaturated limbs.
 //
 // Replaces, on the GPU, the reference's generated per-field C:
 //   <C>_Fp_mont_{add,sub,neg,mul,sqr} / <C>_Fr_mont_*  (lib/cbits/curves/fields/mont/
 //   bls12_381_Fp_mont.c:44-215, bls12_381_Fr_mont.c:44-199, bn128_*_mont.c same lines)
 //   and the bigint256/384 limb kernels under them (lib/cbits/bigint/bigint256.c:108-356).
 //
-// Representation: the SAME Montgomery representation as the reference (R = 2^(64*n64):
-// 2^256 for BN128 Fp/Fr and BLS12-381 Fr, 2^384 for BLS12-381 Fp), stored as 2*n64
-// little-endian 32-bit limbs in registers -- the natural VALU word on CDNA4
-// (v_mad_u64_u32 gives a 32x32+64 -> 64 product-accumulate in one instruction).
-// Every operation returns the canonical representative (< p) for canonical inputs,
-// exactly like the reference (sub_prime_if_above / add-prime-on-borrow, Fr_mont.c:72-116),
-// so results are bit-identical regardless of the algorithm that produced them.
+// Why unsaturated: on CDNA4 `v_mad_u64_u32` (32x32 + 64 -> 64) issues at close to the
+// plain-add rate (tools/microbench/field_rates.hip: 25 Tops/s vs 32), so the cheapest
+// multiprecision product is one mad per limb product with NO carry handling.  With limbs
+// of RB = 28/29 bits a whole product-scanning column (<= 2N products of < 2^(2RB)) fits
+// in one 64-bit accumulator.  Measured: 70 vs 39 G mul/s (381-bit) over 32-bit CIOS.
 //
-// Multiplication is the "no-carry" CIOS variant: valid because every one of the four
-// primes leaves its top 32-bit limb below (2^32-1)/2 (spare bits: BN 2, BLS-Fr 1, BLS-Fp 3).
+//   field          limbs x bits   internal Montgomery radix R'
+//   BN128 Fp, Fr    9 x 29        2^261
+//   BLS12-381 Fr    9 x 29        2^261
+//   BLS12-381 Fp   14 x 28        2^392
+//
+// Values: normalized limbs (< 2^RB), integer value < 2p, Montgomery form w.r.t. R'.
+// The reference's representation (R = 2^256 / 2^384, u64 limbs, canonical) is used
+// at every HBM boundary: fe_load_ref/fe_store_ref repack the bits, fe_to_int /
+// fe_to_ref convert between R and R' with one product by a constant (KIN, KOUT).
+// For linear maps (the NTT) no radix conversion is needed at all: a reference-form
+// value x*R multiplied by an internal-form twiddle w*R' yields (x w)*R.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,26 +29,31 @@
 
 namespace zk {
 
-// ---------------------------------------------------------------------------
-// Field descriptors (compile-time constants; indices are always unrolled so the
-// limbs of p become scalar operands / inline constants, never memory loads).
-
-#define ZK_DEFINE_FIELD(NAME, PFX)                                                  \
-  struct NAME {                                                                     \
-    static constexpr int N = PFX##_N32;     /* 32-bit limbs */                      \
-    static constexpr int N64 = PFX##_N64;                                           \
-    static constexpr int BITS = PFX##_BITS;                                         \
-    static constexpr uint32_t MINV = PFX##_MINV32;                                  \
-    __host__ __device__ static constexpr uint32_t p(int i) {                        \
-      constexpr uint32_t P_[] = PFX##_P32; return P_[i]; }                          \
-    __host__ __device__ static constexpr uint32_t one(int i) {                      \
-      constexpr uint32_t R_[] = PFX##_R32; return R_[i]; }                          \
-    __host__ __device__ static constexpr uint32_t r2(int i) {                       \
-      constexpr uint32_t R2_[] = PFX##_R2_32; return R2_[i]; }                      \
+#define ZK_DEFINE_FIELD(NAME, PFX)                                                      \
+  struct NAME {                                                                         \
+    static constexpr int N = PFX##_U_N;      /* limbs */                                \
+    static constexpr int RB = PFX##_U_RB;    /* bits per limb */                        \
+    static constexpr uint32_t MASK = (1u << PFX##_U_RB) - 1;                            \
+    static constexpr uint32_t MINV = PFX##_U_MINV;                                      \
+    static constexpr int N64 = PFX##_N64;    /* reference u64 limbs */                  \
+    static constexpr int NW = 2 * PFX##_N64; /* reference u32 words */                  \
+    static constexpr int SN = (PFX##_U_N + 3) & ~3; /* storage stride (u32) */          \
+    __host__ __device__ static constexpr uint32_t p(int i) {                            \
+      constexpr uint32_t v_[] = PFX##_U_P; return v_[i]; }                              \
+    __host__ __device__ static constexpr uint32_t p2(int i) {                           \
+      constexpr uint32_t v_[] = PFX##_U_P2; return v_[i]; }                             \
+    __host__ __device__ static constexpr uint32_t one(int i) {                          \
+      constexpr uint32_t v_[] = PFX##_U_ONE; return v_[i]; }                            \
+    __host__ __device__ static constexpr uint32_t kin(int i) {                          \
+      constexpr uint32_t v_[] = PFX##_U_KIN; return v_[i]; }                            \
+    __host__ __device__ static constexpr uint32_t kout(int i) {                         \
+      constexpr uint32_t v_[] = PFX##_U_KOUT; return v_[i]; }                           \
+    __host__ __device__ static constexpr uint32_t kstd(int i) {                         \
+      constexpr uint32_t v_[] = PFX##_U_KSTD; return v_[i]; }                           \
   };
 
-ZK_DEFINE_FIELD(BN_Fp,  ZK_BN128_FP)
-ZK_DEFINE_FIELD(BN_Fr,  ZK_BN128_FR)
+ZK_DEFINE_FIELD(BN_Fp, ZK_BN128_FP)
+ZK_DEFINE_FIELD(BN_Fr, ZK_BN128_FR)
 ZK_DEFINE_FIELD(BLS_Fp, ZK_BLS12_381_FP)
 ZK_DEFINE_FIELD(BLS_Fr, ZK_BLS12_381_FR)
 
@@ -50,21 +62,7 @@ struct Fe {
   uint32_t v[F::N];
 };
 
-// ---------------------------------------------------------------------------
-// limb-level helpers
-
-__device__ __forceinline__ uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t &cout) {
-  uint32_t c;
-  uint32_t r = __builtin_addc(a, b, cin, &c);
-  cout = c;
-  return r;
-}
-__device__ __forceinline__ uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t &bout) {
-  uint32_t c;
-  uint32_t r = __builtin_subc(a, b, bin, &c);
-  bout = c;
-  return r;
-}
+// ---------------------------------------------------------------------------- basics
 
 template <class F>
 __device__ __forceinline__ void fe_zero(Fe<F> &r) {
@@ -72,117 +70,78 @@ __device__ __forceinline__ void fe_zero(Fe<F> &r) {
   for (int i = 0; i < F::N; i++) r.v[i] = 0;
 }
 template <class F>
-__device__ __forceinline__ void fe_one(Fe<F> &r) {
+__device__ __forceinline__ void fe_one(Fe<F> &r) {  // internal-form 1 (R' mod p)
 #pragma unroll
   for (int i = 0; i < F::N; i++) r.v[i] = F::one(i);
 }
 template <class F>
+__device__ __forceinline__ void fe_const_kin(Fe<F> &r) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = F::kin(i);
+}
+// value == 0 (mod p), for values < 2p
+template <class F>
 __device__ __forceinline__ bool fe_is_zero(const Fe<F> &a) {
-  uint32_t acc = 0;
+  uint32_t z = 0, q = 0;
 #pragma unroll
-  for (int i = 0; i < F::N; i++) acc |= a.v[i];
-  return acc == 0;
-}
-template <class F>
-__device__ __forceinline__ bool fe_eq(const Fe<F> &a, const Fe<F> &b) {
-  uint32_t acc = 0;
-#pragma unroll
-  for (int i = 0; i < F::N; i++) acc |= (a.v[i] ^ b.v[i]);
-  return acc == 0;
+  for (int i = 0; i < F::N; i++) {
+    z |= a.v[i];
+    q |= a.v[i] ^ F::p(i);
+  }
+  return z == 0 || q == 0;
 }
 
-// r = (a >= p) ? a - p : a      (a < 2p assumed)
-template <class F>
-__device__ __forceinline__ void fe_reduce_once(Fe<F> &a) {
-  uint32_t t[F::N];
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < F::N; i++) t[i] = subb(a.v[i], F::p(i), br, br);
-  // br == 1  <=> a < p  -> keep a
-#pragma unroll
-  for (int i = 0; i < F::N; i++) a.v[i] = br ? a.v[i] : t[i];
-}
-
+// r = a + b  (mod 2p representative: result < 2p).  Two carry chains (a+b and
+// a+b-2p) run interleaved; the sign of the second selects.
 template <class F>
 __device__ __forceinline__ void fe_add(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
-  uint32_t c = 0;
+  int32_t c0 = 0, c1 = 0;
+  uint32_t s0[F::N], s1[F::N];
 #pragma unroll
-  for (int i = 0; i < F::N; i++) r.v[i] = addc(a.v[i], b.v[i], c, c);
-  // spare top bit => no carry out of the top limb
-  fe_reduce_once(r);
+  for (int i = 0; i < F::N; i++) {
+    const int32_t t = (int32_t)(a.v[i] + b.v[i]);
+    const int32_t v0 = t + c0;
+    const int32_t v1 = t - (int32_t)F::p2(i) + c1;
+    s0[i] = (uint32_t)v0 & F::MASK;
+    s1[i] = (uint32_t)v1 & F::MASK;
+    c0 = v0 >> F::RB;
+    c1 = v1 >> F::RB;
+  }
+  const bool ge = c1 >= 0;  // a + b >= 2p
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = ge ? s1[i] : s0[i];
 }
 
+// r = a - b  (result < 2p): a-b if >= 0 else a-b+2p
 template <class F>
 __device__ __forceinline__ void fe_sub(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
-  uint32_t br = 0;
+  int32_t c0 = 0, c1 = 0;
+  uint32_t s0[F::N], s1[F::N];
 #pragma unroll
-  for (int i = 0; i < F::N; i++) r.v[i] = subb(a.v[i], b.v[i], br, br);
-  const uint32_t mask = 0u - br;
-  uint32_t c = 0;
+  for (int i = 0; i < F::N; i++) {
+    const int32_t t = (int32_t)a.v[i] - (int32_t)b.v[i];
+    const int32_t v0 = t + c0;
+    const int32_t v1 = t + (int32_t)F::p2(i) + c1;
+    s0[i] = (uint32_t)v0 & F::MASK;
+    s1[i] = (uint32_t)v1 & F::MASK;
+    c0 = v0 >> F::RB;
+    c1 = v1 >> F::RB;
+  }
+  const bool neg = c0 < 0;
 #pragma unroll
-  for (int i = 0; i < F::N; i++) r.v[i] = addc(r.v[i], F::p(i) & mask, c, c);
+  for (int i = 0; i < F::N; i++) r.v[i] = neg ? s1[i] : s0[i];
 }
 
 template <class F>
 __device__ __forceinline__ void fe_neg(Fe<F> &r, const Fe<F> &a) {
-  // p - a, and 0 -> 0 (reference: Fr_mont.c:44-58)
-  const uint32_t nz = fe_is_zero(a) ? 0u : 0xffffffffu;
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < F::N; i++) r.v[i] = subb(F::p(i) & nz, a.v[i], br, br);
+  Fe<F> z;
+  fe_zero(z);
+  fe_sub(r, z, a);
 }
 
 template <class F>
 __device__ __forceinline__ void fe_dbl(Fe<F> &r, const Fe<F> &a) { fe_add(r, a, a); }
 
-// Montgomery product, "no-carry" CIOS with 32-bit limbs.
-//   t = a*b*2^(-32N) mod p, canonical.
-template <class F>
-__device__ __forceinline__ void fe_mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
-  constexpr int N = F::N;
-  uint32_t t[N];
-#pragma unroll
-  for (int j = 0; j < N; j++) t[j] = 0;
-#pragma unroll
-  for (int i = 0; i < N; i++) {
-    const uint32_t bi = b.v[i];
-    uint64_t x = (uint64_t)a.v[0] * bi + t[0];
-    uint32_t A = (uint32_t)(x >> 32);
-    const uint32_t t0 = (uint32_t)x;
-    const uint32_t m = t0 * F::MINV;
-    uint64_t y = (uint64_t)m * F::p(0) + t0;
-    uint32_t C = (uint32_t)(y >> 32);
-#pragma unroll
-    for (int j = 1; j < N; j++) {
-      x = (uint64_t)a.v[j] * bi + t[j];
-      x += A;
-      A = (uint32_t)(x >> 32);
-      y = (uint64_t)m * F::p(j) + (uint32_t)x;
-      y += C;
-      C = (uint32_t)(y >> 32);
-      t[j - 1] = (uint32_t)y;
-    }
-    t[N - 1] = C + A;
-  }
-#pragma unroll
-  for (int j = 0; j < N; j++) r.v[j] = t[j];
-  fe_reduce_once(r);
-}
-
-template <class F>
-__device__ __forceinline__ void fe_sqr(Fe<F> &r, const Fe<F> &a) { fe_mul(r, a, a); }
-
-// REDC of a single-width value: a * R^-1 mod p  (the reference's `to_std`,
-// Fr_mont.c:330-335: REDC of [a, 0]; canonical for every a < 2^(32N)).
-template <class F>
-__device__ __forceinline__ void fe_from_mont(Fe<F> &r, const Fe<F> &a) {
-  Fe<F> one;
-#pragma unroll
-  for (int i = 0; i < F::N; i++) one.v[i] = (i == 0) ? 1u : 0u;
-  fe_mul(r, a, one);
-}
-
-// small-integer multiples used by the curve formulas
 template <class F>
 __device__ __forceinline__ void fe_mul3(Fe<F> &r, const Fe<F> &a) {
   Fe<F> t;
@@ -190,29 +149,204 @@ __device__ __forceinline__ void fe_mul3(Fe<F> &r, const Fe<F> &a) {
   fe_add(r, t, a);
 }
 
-// ---------------------------------------------------------------------------
-// memory helpers: limbs are stored in HBM as little-endian u64 words, which is
-// byte-identical to little-endian u32 limbs.
-
+// Montgomery product w.r.t. R' = 2^(RB*N): product scanning (FIPS) with one 64-bit
+// column accumulator; every limb product is a single v_mad_u64_u32.
+// Inputs < 2p (normalized limbs) -> output < 2p (normalized), since 4p < R'.
 template <class F>
-__device__ __forceinline__ void fe_load(Fe<F> &r, const uint64_t *__restrict__ p) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+__device__ __forceinline__ void fe_mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  constexpr int N = F::N;
+  uint32_t m[N];
+  uint32_t o[N];
+  uint64_t acc = 0;
 #pragma unroll
-  for (int i = 0; i < F::N / 4; i++) {
-    uint4 w = q[i];
-    r.v[4 * i + 0] = w.x;
-    r.v[4 * i + 1] = w.y;
-    r.v[4 * i + 2] = w.z;
-    r.v[4 * i + 3] = w.w;
+  for (int k = 0; k < N; k++) {
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+      acc += (uint64_t)a.v[i] * b.v[k - i];
+      acc += (uint64_t)m[i] * F::p(k - i);
+    }
+    acc += (uint64_t)a.v[k] * b.v[0];
+    m[k] = ((uint32_t)acc * F::MINV) & F::MASK;
+    acc += (uint64_t)m[k] * F::p(0);
+    acc >>= F::RB;
+  }
+#pragma unroll
+  for (int k = N; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = k - N + 1; i < N; i++) {
+      acc += (uint64_t)a.v[i] * b.v[k - i];
+      acc += (uint64_t)m[i] * F::p(k - i);
+    }
+    o[k - N] = (uint32_t)acc & F::MASK;
+    acc >>= F::RB;
+  }
+  o[N - 1] = (uint32_t)acc;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = o[i];
+}
+
+// squaring: off-diagonal products once, doubled (saves ~N^2/2 mads)
+template <class F>
+__device__ __forceinline__ void fe_sqr(Fe<F> &r, const Fe<F> &a) {
+  constexpr int N = F::N;
+  uint32_t a2[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) a2[i] = a.v[i] << 1;
+  uint32_t m[N];
+  uint32_t o[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    // a-part of column k: sum_{i<j, i+j=k} 2 a_i a_j  +  a_{k/2}^2
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const int j = k - i;
+      if (j > i && j < N) acc += (uint64_t)a2[i] * a.v[j];
+    }
+    if ((k & 1) == 0 && (k >> 1) < N) acc += (uint64_t)a.v[k >> 1] * a.v[k >> 1];
+    // m-part
+    if (k < N) {
+#pragma unroll
+      for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * F::p(k - i);
+      m[k] = ((uint32_t)acc * F::MINV) & F::MASK;
+      acc += (uint64_t)m[k] * F::p(0);
+      acc >>= F::RB;
+    } else {
+#pragma unroll
+      for (int i = k - N + 1; i < N; i++) acc += (uint64_t)m[i] * F::p(k - i);
+      o[k - N] = (uint32_t)acc & F::MASK;
+      acc >>= F::RB;
+    }
+  }
+  o[N - 1] = (uint32_t)acc;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = o[i];
+}
+
+// canonical representative (< p) of a value < 2p
+template <class F>
+__device__ __forceinline__ void fe_canon(Fe<F> &a) {
+  int32_t c = 0;
+  uint32_t d[F::N];
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {
+    const int32_t v = (int32_t)a.v[i] - (int32_t)F::p(i) + c;
+    d[i] = (uint32_t)v & F::MASK;
+    c = v >> F::RB;
+  }
+  const bool lt = c < 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) a.v[i] = lt ? a.v[i] : d[i];
+}
+
+// ---------------------------------------------------------------------------- radix conversion
+
+// reference Montgomery (R) -> internal (R'):  x*R  ->  x*R'
+template <class F>
+__device__ __forceinline__ void fe_to_int(Fe<F> &r, const Fe<F> &a) {
+  Fe<F> k;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) k.v[i] = F::kin(i);
+  fe_mul(r, a, k);
+}
+// internal (R') -> reference Montgomery (R), canonical
+template <class F>
+__device__ __forceinline__ void fe_to_ref(Fe<F> &r, const Fe<F> &a) {
+  Fe<F> k;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) k.v[i] = F::kout(i);
+  fe_mul(r, a, k);
+  fe_canon(r);
+}
+// reference Montgomery -> standard integer (the reference's `to_std` = REDC(x, 0),
+// Fr_mont.c:330-335), canonical; valid for every 256-bit input x (a raw bit pattern).
+template <class F>
+__device__ __forceinline__ void fe_ref_to_std(Fe<F> &r, const Fe<F> &a) {
+  Fe<F> k;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) k.v[i] = F::kstd(i);
+  fe_mul(r, a, k);
+  fe_canon(r);
+}
+
+// ---------------------------------------------------------------------------- packing
+
+// NW little-endian u32 words (any integer < 2^(32 NW)) -> RB-bit limbs
+template <class F>
+__device__ __forceinline__ void fe_unpack(Fe<F> &r, const uint32_t *w) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {
+    const int bit = i * F::RB;
+    const int wi = bit >> 5, sh = bit & 31;
+    uint32_t lo = (wi < F::NW) ? w[wi] : 0u;
+    uint32_t hi = (wi + 1 < F::NW) ? w[wi + 1] : 0u;
+    uint32_t x = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+    r.v[i] = x & F::MASK;
   }
 }
+// RB-bit limbs (value < 2^(32 NW)) -> NW u32 words
 template <class F>
-__device__ __forceinline__ void fe_store(uint64_t *__restrict__ p, const Fe<F> &a) {
+__device__ __forceinline__ void fe_pack(uint32_t *w, const Fe<F> &a) {
+#pragma unroll
+  for (int j = 0; j < F::NW; j++) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) {
+      const int lo = i * F::RB;           // limb i covers bits [lo, lo+RB)
+      const int wlo = j * 32;             // word j covers bits [wlo, wlo+32)
+      if (lo + F::RB <= wlo || lo >= wlo + 32) continue;
+      const int sh = lo - wlo;
+      x |= sh >= 0 ? (a.v[i] << sh) : (a.v[i] >> (-sh));
+    }
+    w[j] = x;
+  }
+}
+
+// load / store a reference-form element (N64 u64 words in HBM)
+template <class F>
+__device__ __forceinline__ void fe_load_ref(Fe<F> &r, const uint64_t *__restrict__ p) {
+  uint32_t w[F::NW];
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+  for (int i = 0; i < F::NW / 4; i++) {
+    uint4 x = q[i];
+    w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
+  }
+  fe_unpack(r, w);
+}
+// stores the canonical representative
+template <class F>
+__device__ __forceinline__ void fe_store_ref(uint64_t *__restrict__ p, const Fe<F> &a) {
+  Fe<F> c = a;
+  fe_canon(c);
+  uint32_t w[F::NW];
+  fe_pack(w, c);
   uint4 *q = reinterpret_cast<uint4 *>(p);
 #pragma unroll
-  for (int i = 0; i < F::N / 4; i++) {
-    q[i] = make_uint4(a.v[4 * i + 0], a.v[4 * i + 1], a.v[4 * i + 2], a.v[4 * i + 3]);
+  for (int i = 0; i < F::NW / 4; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// internal-form storage: SN u32 words (limbs, zero padded), 16-B aligned
+template <class F>
+__device__ __forceinline__ void fe_load_u(Fe<F> &r, const uint32_t *__restrict__ p) {
+  const uint4 *q = reinterpret_cast<const uint4 *>(p);
+  uint32_t w[F::SN];
+#pragma unroll
+  for (int i = 0; i < F::SN / 4; i++) {
+    uint4 x = q[i];
+    w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
   }
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = w[i];
+}
+template <class F>
+__device__ __forceinline__ void fe_store_u(uint32_t *__restrict__ p, const Fe<F> &a) {
+  uint32_t w[F::SN];
+#pragma unroll
+  for (int i = 0; i < F::SN; i++) w[i] = i < F::N ? a.v[i] : 0u;
+  uint4 *q = reinterpret_cast<uint4 *>(p);
+#pragma unroll
+  for (int i = 0; i < F::SN / 4; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
 }  // namespace zk

@@ -35,20 +35,32 @@ namespace zk {
 // XYZZ storage: 4 consecutive field elements, F::N u32 words each.
 template <class F>
 __device__ __forceinline__ void xyzz_store(uint32_t *p, const Xyzz<F> &a) {
-  fe_store(reinterpret_cast<uint64_t *>(p + 0 * F::N), a.X);
-  fe_store(reinterpret_cast<uint64_t *>(p + 1 * F::N), a.Y);
-  fe_store(reinterpret_cast<uint64_t *>(p + 2 * F::N), a.ZZ);
-  fe_store(reinterpret_cast<uint64_t *>(p + 3 * F::N), a.ZZZ);
+  fe_store_u(p + 0 * F::SN, a.X);
+  fe_store_u(p + 1 * F::SN, a.Y);
+  fe_store_u(p + 2 * F::SN, a.ZZ);
+  fe_store_u(p + 3 * F::SN, a.ZZZ);
 }
 template <class F>
 __device__ __forceinline__ void xyzz_load(Xyzz<F> &a, const uint32_t *p) {
-  fe_load(a.X, reinterpret_cast<const uint64_t *>(p + 0 * F::N));
-  fe_load(a.Y, reinterpret_cast<const uint64_t *>(p + 1 * F::N));
-  fe_load(a.ZZ, reinterpret_cast<const uint64_t *>(p + 2 * F::N));
-  fe_load(a.ZZZ, reinterpret_cast<const uint64_t *>(p + 3 * F::N));
+  fe_load_u(a.X, p + 0 * F::SN);
+  fe_load_u(a.Y, p + 1 * F::SN);
+  fe_load_u(a.ZZ, p + 2 * F::SN);
+  fe_load_u(a.ZZZ, p + 3 * F::SN);
 }
 template <class F>
-constexpr int xyzz_words() { return 4 * F::N; }
+constexpr int xyzz_words() { return 4 * F::SN; }
+template <class F>
+constexpr int aff_words() { return 2 * F::SN; }
+
+// 0. affine points: reference form -> internal form (once per call)
+template <class C>
+__global__ void __launch_bounds__(256) k_points_int(const uint64_t *__restrict__ pts, int n,
+                                                    uint32_t *__restrict__ out) {
+  using F = typename C::Fp;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  aff_ref_to_int<F>(out + (size_t)i * aff_words<F>(), pts + (size_t)i * 2 * F::N64);
+}
 
 // ---------------------------------------------------------------------------
 // 1. digits + histogram
@@ -61,25 +73,19 @@ __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ sca
   using Fr = typename C::Fr;
   uint32_t k[9];
   {
-    Fe<Fr> s;
-    if (nl == 4) {
-      fe_load(s, scalars + (size_t)i * 4);
-    } else {  // std scalars of 1..3 limbs: zero-extend
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint64_t w = (j < nl) ? scalars[(size_t)i * nl + j] : 0;
-        s.v[2 * j] = (uint32_t)w;
-        s.v[2 * j + 1] = (uint32_t)(w >> 32);
-      }
+    for (int j = 0; j < 4; j++) {  // std scalars of 1..3 limbs: zero-extended
+      const uint64_t w = (j < nl) ? scalars[(size_t)i * nl + j] : 0;
+      k[2 * j] = (uint32_t)w;
+      k[2 * j + 1] = (uint32_t)(w >> 32);
     }
-    if (mont) {
-      Fe<Fr> t;
-      fe_from_mont(t, s);
-      s = t;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++) k[j] = s.v[j];
     k[8] = 0;
+    if (mont) {  // Montgomery -> standard (REDC), Fr_mont.c:330-335
+      Fe<Fr> s, t;
+      fe_unpack(s, k);
+      fe_ref_to_std(t, s);
+      fe_pack(k, t);
+    }
   }
   const uint32_t B = 1u << (c - 1);
   const uint32_t full = 1u << c;
@@ -131,10 +137,10 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ offse
 }
 
 template <class F>
-__device__ __forceinline__ void load_signed_point(Aff<F> &a, bool &inf, const uint64_t *__restrict__ points,
+__device__ __forceinline__ void load_signed_point(Aff<F> &a, bool &inf, const uint32_t *__restrict__ points,
                                                   uint32_t code) {
   const uint32_t idx = code & 0x7fffffffu;
-  inf = !aff_load(a, points + (size_t)idx * 2 * F::N64);
+  inf = !aff_load(a, points + (size_t)idx * aff_words<F>());
   if (!inf && (code & 0x80000000u)) {
     Fe<F> ny;
     fe_neg(ny, a.y);
@@ -144,7 +150,7 @@ __device__ __forceinline__ void load_signed_point(Aff<F> &a, bool &inf, const ui
 
 // 4. balanced accumulation: thread t owns sorted entries [t*CH, min((t+1)*CH, total))
 template <class C>
-__global__ void __launch_bounds__(256) k_accum(const uint64_t *__restrict__ points,
+__global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ points,
                                                const uint32_t *__restrict__ list,
                                                const uint32_t *__restrict__ offsets, uint32_t nb,
                                                uint32_t total, int CH, uint32_t *__restrict__ buckets,
@@ -292,10 +298,15 @@ __global__ void k_export(const uint32_t *__restrict__ in, int n, uint64_t *__res
   Xyzz<F> p;
   xyzz_load(p, in + (size_t)g * xyzz_words<F>());
   uint64_t *o = out + (size_t)g * 4 * F::N64;
-  fe_store(o + 0 * F::N64, p.X);
-  fe_store(o + 1 * F::N64, p.Y);
-  fe_store(o + 2 * F::N64, p.ZZ);
-  fe_store(o + 3 * F::N64, p.ZZZ);
+  Fe<F> t;
+  fe_to_ref(t, p.X);
+  fe_store_ref(o + 0 * F::N64, t);
+  fe_to_ref(t, p.Y);
+  fe_store_ref(o + 1 * F::N64, t);
+  fe_to_ref(t, p.ZZ);
+  fe_store_ref(o + 2 * F::N64, t);
+  fe_to_ref(t, p.ZZZ);
+  fe_store_ref(o + 3 * F::N64, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -338,7 +349,7 @@ static MsmShape make_shape(int n, int c, int nl) {
 template <class C>
 static size_t workspace_bytes(const MsmShape &s) {
   using F = typename C::Fp;
-  const size_t xw = 4 * F::N * 4;  // bytes per XYZZ
+  const size_t xw = xyzz_words<F>() * 4;  // bytes per XYZZ
   const size_t nb = (size_t)s.W * s.B;
   const size_t maxent = (size_t)s.W * s.n;
   const size_t nchunks = (maxent + s.CH - 1) / s.CH + 1;
@@ -348,6 +359,7 @@ static size_t workspace_bytes(const MsmShape &s) {
   auto add = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
   add((size_t)s.n * 4 * 8);          // staged scalars (<= 4 limbs)
   add((size_t)s.n * 2 * C::NP64 * 8);  // staged points
+  add((size_t)s.n * aff_words<F>() * 4);  // internal-form points
   add(maxent * 4);                   // digits
   add((nb + 1) * 4);                 // counts
   add((nb + 1) * 4);                 // offsets
@@ -396,6 +408,7 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
     d_sc = a;
     d_pt = b;
   }
+  uint32_t *pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
   uint32_t *digits = dev.arena.take<uint32_t>((size_t)s.W * n);
   uint32_t *counts = dev.arena.take<uint32_t>(nb + 1);
   uint32_t *offsets = dev.arena.take<uint32_t>(nb + 1);
@@ -416,6 +429,8 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   void *cubtmp = dev.arena.take<char>(cub);
 
   ZK_CHECK(hipMemsetAsync(counts, 0, (nb + 1) * 4, st));
+  hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_pt, n, pts_int);
+  ZK_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_sc, n, nl, mont ? 1 : 0, c, s.W,
                      digits, counts);
   ZK_CHECK(hipGetLastError());
@@ -431,7 +446,7 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   if (total > 0) {
     const uint32_t nthreads = (total + s.CH - 1) / s.CH;
     if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev0, st));
-    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(nthreads, 256)), dim3(256), 0, st, d_pt, list, offsets,
+    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(nthreads, 256)), dim3(256), 0, st, pts_int, list, offsets,
                        (uint32_t)nb, total, s.CH, buckets, heads, tails);
     ZK_CHECK(hipGetLastError());
     if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev1, st));

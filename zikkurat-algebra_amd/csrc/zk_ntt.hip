@@ -35,9 +35,10 @@ struct PassDesc {
 template <class F>
 __device__ __forceinline__ void twiddle(Fe<F> &w, const uint64_t *__restrict__ tlo, const uint64_t *__restrict__ thi,
                                         int h, uint32_t e) {
+  // tables hold internal-form powers, stored packed (canonical, N64 u64 words)
   Fe<F> a, b;
-  fe_load(a, tlo + (size_t)(e & ((1u << h) - 1)) * F::N64);
-  fe_load(b, thi + (size_t)(e >> h) * F::N64);
+  fe_load_ref(a, tlo + (size_t)(e & ((1u << h) - 1)) * F::N64);
+  fe_load_ref(b, thi + (size_t)(e >> h) * F::N64);
   fe_mul(w, a, b);
 }
 
@@ -110,9 +111,9 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
       addr = pos + k;
     }
     Fe<F> x;
-    fe_load(x, src + addr * F::N64);
-    const int kr = __builtin_bitreverse32((uint32_t)k) >> (32 - r);
-    uint32_t *d = data + ((size_t)g * R + (r ? kr : 0)) * NW;
+    fe_load_ref(x, src + addr * F::N64);
+    const int kr = r ? (int)(__builtin_bitreverse32((uint32_t)k) >> (32 - r)) : 0;
+    uint32_t *d = data + ((size_t)g * R + kr) * NW;
 #pragma unroll
     for (int q = 0; q < NW; q++) d[q] = x.v[q];
   }
@@ -151,7 +152,11 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
 
   // store (with inter-pass twiddle, or to natural positions on the last pass)
   Fe<F> sc;
-  if (last && scale) fe_load(sc, scale);
+  if (last && scale) {
+    Fe<F> t;
+    fe_load_ref(t, scale);
+    fe_to_int(sc, t);
+  }
   for (int e = tid; e < nel; e += NTT_THREADS) {
     int g = e % G, k = e / G;  // consecutive threads -> consecutive g (coalesced)
     Fe<F> x;
@@ -193,7 +198,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
         x = y;
       }
     }
-    fe_store(dst + addr * F::N64, x);
+    fe_store_ref(dst + addr * F::N64, x);
   }
 }
 
@@ -208,24 +213,26 @@ __global__ void k_tw_tables(uint64_t *__restrict__ tlo, uint64_t *__restrict__ t
     fe_one(acc);
     for (int b = 0; b < h; b++)
       if ((i >> b) & 1) {
-        Fe<F> p, t;
-        fe_load(p, pows + (size_t)b * F::N64);
+        Fe<F> p, q, t;
+        fe_load_ref(q, pows + (size_t)b * F::N64);
+        fe_to_int(p, q);
         fe_mul(t, acc, p);
         acc = t;
       }
-    fe_store(tlo + (size_t)i * F::N64, acc);
+    fe_store_ref(tlo + (size_t)i * F::N64, acc);
   }
   if (i < nhi) {
     Fe<F> acc;
     fe_one(acc);
     for (int b = 0; b < m - h; b++)
       if ((i >> b) & 1) {
-        Fe<F> p, t;
-        fe_load(p, pows + (size_t)(b + h) * F::N64);
+        Fe<F> p, q, t;
+        fe_load_ref(q, pows + (size_t)(b + h) * F::N64);
+        fe_to_int(p, q);
         fe_mul(t, acc, p);
         acc = t;
       }
-    fe_store(thi + (size_t)i * F::N64, acc);
+    fe_store_ref(thi + (size_t)i * F::N64, acc);
   }
 }
 
@@ -360,7 +367,7 @@ struct CfgBLS { using Fd = BLS_Fr; using Fh = zkh::BLS_Fr; };
 
 void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst, bool host_io,
          bool inverse) {
-  ZK_REQUIRE(m >= 0 && m <= 32, "ntt: log2 size out of range");
+  ZK_REQUIRE(m >= 0 && m <= 30, "ntt: log2 size out of range (0..30)");
   Device &dev = current_device();
   std::lock_guard<std::mutex> lock(dev.mu);
   if (curve == 0) ntt_run<CfgBN>(dev, m, gen_mont, src, dst, host_io, inverse);

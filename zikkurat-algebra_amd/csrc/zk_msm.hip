@@ -6,14 +6,17 @@
 // identical for points outside the order-r subgroup too), computed with
 // a GPU-shaped schedule:
 //
+//   0. k_points_int affine points -> internal radix (one product per coordinate)
 //   1. k_digits     scalar (Montgomery -> standard by REDC, Fr_mont.c:330-335) ->
-//                   signed c-bit digits for all W windows + per-bucket histogram
-//   2. scan         exclusive scan of the W*B bucket counts (hipCUB)
-//   3. k_scatter    counting-sort scatter: (point index | sign) into bucket order
+//                   signed c-bit digits for all W windows -> (bucket key, index|sign)
+//   2. sort         LSD radix sort of the W*n pairs by bucket key (hipCUB onesweep)
+//   3. k_offsets    bucket start offsets from the sorted keys
 //   4. k_accum      balanced bucket accumulation: every thread adds exactly CH
 //                   consecutive sorted entries (mixed XYZZ += affine adds), flushing
-//                   complete buckets directly and boundary runs to head/tail slots
-//   5. k_fixup      stitches buckets that straddle chunks
+//                   complete runs to their bucket and boundary runs as partial items
+//   5. k_stitch     partial items are compacted and summed per bucket with the same
+//                   balanced scheme, level after level (log_{SCH/2} levels): no serial
+//                   loop anywhere, so skewed scalars (all equal, carry windows) stay fast
 //   6. k_seg        per (window, segment of L buckets): T = sum B_m, R = sum (m-lo+1) B_m
 //   7. k_bitsum     sum_m m B_m = sum_s R_s + L * sum_k 2^k U_k, U_k = sum_{s: bit k} T_s:
 //                   every term is a plain point sum -> wide, shallow reductions
@@ -63,11 +66,13 @@ __global__ void __launch_bounds__(256) k_points_int(const uint64_t *__restrict__
 }
 
 // ---------------------------------------------------------------------------
-// 1. digits + histogram
+// 1. digits -> (key, value) pairs for the bucket sort.
+//    key = w * B + (|digit| - 1), or nb (sentinel, sorts last) for a zero digit
+//    value = point index | sign << 31
 template <class C>
 __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int nl, int mont,
-                                                int c, int W, uint32_t *__restrict__ digits,
-                                                uint32_t *__restrict__ counts) {
+                                                int c, int W, uint32_t *__restrict__ keys,
+                                                uint32_t *__restrict__ vals) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   using Fr = typename C::Fr;
@@ -90,40 +95,40 @@ __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ sca
   const uint32_t B = 1u << (c - 1);
   const uint32_t full = 1u << c;
   const uint32_t mask = full - 1;
+  const uint32_t nb = (uint32_t)W * B;
   uint32_t carry = 0;
   for (int w = 0; w < W; w++) {
     uint32_t raw = (k[0] & mask) + carry;
     // shift the 256-bit scalar right by c (c < 32)
 #pragma unroll
     for (int j = 0; j < 8; j++) k[j] = __builtin_amdgcn_alignbit(k[j + 1], k[j], c);
-    uint32_t code = 0;
-    if (raw > B) {
-      code = (full - raw) | 0x80000000u;  // negative digit raw - 2^c  (0 if raw == 2^c)
+    uint32_t mag, sign;
+    if (raw > B) {  // negative digit raw - 2^c (zero when raw == 2^c)
+      mag = full - raw;
+      sign = 0x80000000u;
       carry = 1;
-      if (raw == full) code = 0;
     } else {
-      code = raw;
+      mag = raw;
+      sign = 0;
       carry = 0;
     }
-    digits[(size_t)w * n + i] = code;
-    if (code) atomicAdd(&counts[(size_t)w * B + (code & 0x7fffffffu) - 1], 1u);
+    keys[(size_t)w * n + i] = mag ? (uint32_t)w * B + mag - 1 : nb;
+    vals[(size_t)w * n + i] = (uint32_t)i | sign;
   }
 }
 
-// 3. counting-sort scatter
-__global__ void __launch_bounds__(256) k_scatter(const uint32_t *__restrict__ digits, int n, int c, int W,
-                                                 uint32_t *__restrict__ cursor, uint32_t *__restrict__ list) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t B = 1u << (c - 1);
-  for (int w = 0; w < W; w++) {
-    uint32_t code = digits[(size_t)w * n + i];
-    if (code) {
-      uint32_t b = (uint32_t)w * B + (code & 0x7fffffffu) - 1;
-      uint32_t pos = atomicAdd(&cursor[b], 1u);
-      list[pos] = (uint32_t)i | (code & 0x80000000u);
-    }
+// 3. bucket offsets from the sorted keys: offsets[b] = first position with key >= b,
+//    one binary search per bucket (no serial loops, whatever the key distribution)
+__global__ void __launch_bounds__(256) k_offsets(const uint32_t *__restrict__ skeys, uint32_t M, uint32_t nb,
+                                                 uint32_t *__restrict__ offsets) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nb) return;
+  uint32_t lo = 0, hi = M;  // first index in [lo, hi] with key >= b
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (skeys[mid] < b) lo = mid + 1; else hi = mid;
   }
+  offsets[b] = lo;
 }
 
 // first bucket index b with offsets[b+1] > e  (offsets has nb+1 entries)
@@ -148,77 +153,143 @@ __device__ __forceinline__ void load_signed_point(Aff<F> &a, bool &inf, const ui
   }
 }
 
-// 4. balanced accumulation: thread t owns sorted entries [t*CH, min((t+1)*CH, total))
+// 4. level-0 balanced accumulation: thread t owns sorted entries [t*CH, min((t+1)*CH, total)).
+//    Runs of one bucket that lie entirely inside the chunk are written straight to
+//    buckets[b]; a run that crosses the chunk boundary (the chunk's first and/or last run)
+//    becomes a "partial item" (key b, XYZZ sum) in slot 2t / 2t+1 of the item arrays.
+//    Item slots that stay empty carry key = nb (dropped by the compaction).
 template <class C>
 __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ points,
                                                const uint32_t *__restrict__ list,
                                                const uint32_t *__restrict__ offsets, uint32_t nb,
-                                               uint32_t total, int CH, uint32_t *__restrict__ buckets,
-                                               uint32_t *__restrict__ heads, uint32_t *__restrict__ tails) {
+                                               int CH, uint32_t *__restrict__ buckets,
+                                               uint32_t *__restrict__ ikeys, uint32_t *__restrict__ ivals,
+                                               uint32_t nslots) {
   using F = typename C::Fp;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * t >= nslots) return;
+  const uint32_t total = offsets[nb];
   const uint32_t cs = t * (uint32_t)CH;
-  if (cs >= total) return;
-  const uint32_t ce = min(total, cs + (uint32_t)CH);
-  uint32_t b = bucket_of(offsets, nb, cs);
-  uint32_t bend = offsets[b + 1];
-  bool first_run = true;
-  Xyzz<F> acc;
-  xyzz_set_inf(acc);
-  for (uint32_t e = cs; e < ce; e++) {
-    if (e >= bend) {
-      // flush the run of bucket b
-      if (first_run) xyzz_store(heads + (size_t)t * xyzz_words<F>(), acc);
-      else xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);  // complete inside the chunk
-      first_run = false;
-      xyzz_set_inf(acc);
-      do { b++; bend = offsets[b + 1]; } while (bend <= e);
+  uint32_t k0 = nb, k1 = nb;  // item keys of slots 2t, 2t+1
+  if (cs < total) {
+    const uint32_t ce = min(total, cs + (uint32_t)CH);
+    uint32_t b = bucket_of(offsets, nb, cs);
+    uint32_t bbeg = offsets[b], bend = offsets[b + 1];
+    bool first_run = true;
+    Xyzz<F> acc;
+    xyzz_set_inf(acc);
+    for (uint32_t e = cs; e < ce; e++) {
+      if (e >= bend) {  // run of bucket b ends inside the chunk
+        if (first_run && bbeg < cs) {
+          xyzz_store(ivals + (size_t)(2 * t) * xyzz_words<F>(), acc);
+          k0 = b;
+        } else {
+          xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+        }
+        first_run = false;
+        xyzz_set_inf(acc);
+        do { b++; bbeg = offsets[b]; bend = offsets[b + 1]; } while (bend <= e);
+      }
+      Aff<F> P;
+      bool inf;
+      load_signed_point(P, inf, points, list[e]);
+      if (!inf) xyzz_add_aff(acc, P);
     }
-    Aff<F> P;
-    bool inf;
-    load_signed_point(P, inf, points, list[e]);
-    if (!inf) xyzz_add_aff(acc, P);
+    // last run: partial if it started before the chunk or continues after it
+    if (bbeg < cs || bend > ce) {
+      const uint32_t slot = first_run ? 2 * t : 2 * t + 1;
+      xyzz_store(ivals + (size_t)slot * xyzz_words<F>(), acc);
+      if (first_run) k0 = b; else k1 = b;
+    } else {
+      xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+    }
   }
-  // last run
-  if (first_run) xyzz_store(heads + (size_t)t * xyzz_words<F>(), acc);
-  else if (bend > ce) xyzz_store(tails + (size_t)t * xyzz_words<F>(), acc);
-  else xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+  ikeys[2 * t] = k0;
+  ikeys[2 * t + 1] = k1;
 }
 
-// 5. stitch buckets that straddle chunks; write infinity into empty buckets
+// 5a. compaction of the partial items (keys < nb), order preserving: scatter by a
+//     prefix sum of the valid flags (scan done by hipCUB on `flags`)
+__global__ void __launch_bounds__(256) k_item_flags(const uint32_t *__restrict__ ikeys, const uint32_t *__restrict__ count,
+                                                    uint32_t nslots_max, uint32_t nb, uint32_t *__restrict__ flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots_max) return;
+  const uint32_t n = count ? *count : nslots_max;
+  flags[i] = (i < n && ikeys[i] < nb) ? 1u : 0u;
+}
 template <class C>
-__global__ void __launch_bounds__(256) k_fixup(const uint32_t *__restrict__ offsets, uint32_t nb, int CH,
-                                               uint32_t *__restrict__ buckets,
-                                               const uint32_t *__restrict__ heads,
-                                               const uint32_t *__restrict__ tails) {
+__global__ void __launch_bounds__(256) k_item_compact(const uint32_t *__restrict__ ikeys, const uint32_t *__restrict__ ivals,
+                                                      const uint32_t *__restrict__ flags, const uint32_t *__restrict__ pos,
+                                                      uint32_t nslots_max, uint32_t *__restrict__ okeys,
+                                                      uint32_t *__restrict__ ovals, uint32_t *__restrict__ ocount) {
   using F = typename C::Fp;
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nb) return;
-  const uint32_t ob = offsets[b], oe = offsets[b + 1];
-  Xyzz<F> acc;
-  if (ob == oe) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots_max) return;
+  if (i == nslots_max - 1) *ocount = pos[i] + flags[i];
+  if (!flags[i]) return;
+  const uint32_t o = pos[i];
+  okeys[o] = ikeys[i];
+  const uint4 *s = reinterpret_cast<const uint4 *>(ivals + (size_t)i * xyzz_words<F>());
+  uint4 *d = reinterpret_cast<uint4 *>(ovals + (size_t)o * xyzz_words<F>());
+#pragma unroll
+  for (int q = 0; q < xyzz_words<F>() / 4; q++) d[q] = s[q];
+}
+
+// 5b. stitch level: the compacted items (sorted by key) are summed per key with the
+//     same balanced-chunk scheme; complete runs go to buckets[b], runs crossing a chunk
+//     boundary become the next level's items.  Levels repeat until one chunk remains.
+template <class C>
+__global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                const uint32_t *__restrict__ count, uint32_t nb, int CH,
+                                                uint32_t *__restrict__ buckets, uint32_t *__restrict__ okeys,
+                                                uint32_t *__restrict__ ovals, uint32_t nslots) {
+  using F = typename C::Fp;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * t >= nslots) return;
+  const uint32_t M = *count;
+  const uint32_t cs = t * (uint32_t)CH;
+  uint32_t k0 = nb, k1 = nb;
+  if (cs < M) {
+    const uint32_t ce = min(M, cs + (uint32_t)CH);
+    uint32_t b = keys[cs];
+    const bool cont_in = cs > 0 && keys[cs - 1] == b;
+    bool first_run = true;
+    Xyzz<F> acc;
     xyzz_set_inf(acc);
-    xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
-    return;
+    for (uint32_t e = cs; e < ce; e++) {
+      const uint32_t k = keys[e];
+      if (k != b) {
+        if (first_run && cont_in) {
+          xyzz_store(ovals + (size_t)(2 * t) * xyzz_words<F>(), acc);
+          k0 = b;
+        } else {
+          xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+        }
+        first_run = false;
+        xyzz_set_inf(acc);
+        b = k;
+      }
+      Xyzz<F> v;
+      xyzz_load(v, vals + (size_t)e * xyzz_words<F>());
+      xyzz_add(acc, v);
+    }
+    const bool cont_out = ce < M && keys[ce] == b;
+    if ((first_run && cont_in) || cont_out) {
+      const uint32_t slot = first_run ? 2 * t : 2 * t + 1;
+      xyzz_store(ovals + (size_t)slot * xyzz_words<F>(), acc);
+      if (first_run) k0 = b; else k1 = b;
+    } else {
+      xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+    }
   }
-  const uint32_t t0 = ob / (uint32_t)CH, t1 = (oe - 1) / (uint32_t)CH;
-  if (ob == t0 * (uint32_t)CH) {
-    xyzz_load(acc, heads + (size_t)t0 * xyzz_words<F>());
-  } else {
-    if (t1 == t0) return;  // complete inside chunk t0, already written
-    xyzz_load(acc, tails + (size_t)t0 * xyzz_words<F>());
-  }
-  for (uint32_t t = t0 + 1; t <= t1; t++) {
-    Xyzz<F> h;
-    xyzz_load(h, heads + (size_t)t * xyzz_words<F>());
-    xyzz_add(acc, h);
-  }
-  xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+  okeys[2 * t] = k0;
+  okeys[2 * t + 1] = k1;
 }
 
 // 6. per (window, segment): T = sum B_m, R = sum (m - lo + 1) B_m over L buckets
 template <class C>
-__global__ void __launch_bounds__(256) k_seg(const uint32_t *__restrict__ buckets, int W, int B, int L,
+__global__ void __launch_bounds__(256) k_seg(const uint32_t *__restrict__ buckets,
+                                             const uint32_t *__restrict__ offsets, int W, int B, int L,
                                              uint32_t *__restrict__ Tout, uint32_t *__restrict__ Rout) {
   using F = typename C::Fp;
   const int S = B / L;
@@ -229,9 +300,12 @@ __global__ void __launch_bounds__(256) k_seg(const uint32_t *__restrict__ bucket
   xyzz_set_inf(T);
   xyzz_set_inf(R);
   for (int m = L - 1; m >= 0; m--) {
-    Xyzz<F> bm;
-    xyzz_load(bm, buckets + ((size_t)w * B + (size_t)s * L + m) * xyzz_words<F>());
-    xyzz_add(T, bm);
+    const size_t b = (size_t)w * B + (size_t)s * L + m;
+    if (offsets[b + 1] > offsets[b]) {  // empty buckets hold garbage (never written)
+      Xyzz<F> bm;
+      xyzz_load(bm, buckets + b * xyzz_words<F>());
+      xyzz_add(T, bm);
+    }
     xyzz_add(R, T);
   }
   xyzz_store(Tout + (size_t)g * xyzz_words<F>(), T);
@@ -312,8 +386,14 @@ __global__ void k_export(const uint32_t *__restrict__ in, int n, uint64_t *__res
 // ---------------------------------------------------------------------------
 // host orchestration
 
+static int key_bits(size_t nb) {  // keys are in [0, nb]
+  int b = 1;
+  while (((size_t)1 << b) <= nb) b++;
+  return b;
+}
+
 struct MsmShape {
-  int n, c, W, B, L, S, logS, J, CH, CH2, nchunk;
+  int n, c, W, B, L, S, logS, J, CH, CH2, nchunk, SCH;
 };
 
 static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; return r; }
@@ -340,11 +420,15 @@ static MsmShape make_shape(int n, int c, int nl) {
   s.S = s.B / s.L;
   s.logS = ilog2((unsigned)s.S);
   s.J = s.logS + 1;
-  s.CH = 32;
+  s.CH = 64;   // entries per thread in the level-0 accumulation
+  s.SCH = 32;  // items per thread in the stitch levels
   s.CH2 = 16;
   s.nchunk = (s.S + s.CH2 - 1) / s.CH2;
   return s;
 }
+
+static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.n + s.CH - 1) / s.CH); }
+static size_t stitch_slots1(const MsmShape &s) { return 2 * ((stitch_slots0(s) + s.SCH - 1) / s.SCH) + 2; }
 
 template <class C>
 static size_t workspace_bytes(const MsmShape &s) {
@@ -352,25 +436,26 @@ static size_t workspace_bytes(const MsmShape &s) {
   const size_t xw = xyzz_words<F>() * 4;  // bytes per XYZZ
   const size_t nb = (size_t)s.W * s.B;
   const size_t maxent = (size_t)s.W * s.n;
-  const size_t nchunks = (maxent + s.CH - 1) / s.CH + 1;
-  size_t cub = 0;
-  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(nb + 1)));
+  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s);
+  size_t cub = 0, cub2 = 0;
+  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                              (uint32_t *)nullptr, (uint32_t *)nullptr, (int)maxent, 0,
+                                              key_bits(nb)));
+  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)ns0));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-  add((size_t)s.n * 4 * 8);          // staged scalars (<= 4 limbs)
-  add((size_t)s.n * 2 * C::NP64 * 8);  // staged points
+  add((size_t)s.n * 4 * 8);               // staged scalars (<= 4 limbs)
+  add((size_t)s.n * 2 * C::NP64 * 8);     // staged points
   add((size_t)s.n * aff_words<F>() * 4);  // internal-form points
-  add(maxent * 4);                   // digits
-  add((nb + 1) * 4);                 // counts
-  add((nb + 1) * 4);                 // offsets
-  add((nb + 1) * 4);                 // cursor
-  add(maxent * 4);                   // list
-  add(nchunks * xw * 2);             // heads + tails
-  add(nb * xw);                      // buckets
-  add((size_t)s.W * s.S * xw * 2);   // T, R
+  add(maxent * 4 * 4);                    // keys, vals, sorted keys, sorted vals
+  add((nb + 1) * 4);                      // offsets
+  add(ns0 * (xw + 4) * 2 + ns0 * 8 + 64); // level-0 items, compacted items, flags, pos, count
+  add(ns1 * (xw + 4) * 2);                // stitch ping-pong
+  add(nb * xw);                           // buckets
+  add((size_t)s.W * s.S * xw * 2);        // T, R
   add((size_t)s.W * s.J * s.nchunk * xw * 2);  // bitsum + sumseg ping-pong
   add((size_t)s.W * s.J * 4 * C::NP64 * 8);    // export
-  add(cub);
+  add(cub > cub2 ? cub : cub2);
   return bytes + (1 << 20);
 }
 
@@ -409,53 +494,84 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
     d_pt = b;
   }
   uint32_t *pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
-  uint32_t *digits = dev.arena.take<uint32_t>((size_t)s.W * n);
-  uint32_t *counts = dev.arena.take<uint32_t>(nb + 1);
-  uint32_t *offsets = dev.arena.take<uint32_t>(nb + 1);
-  uint32_t *cursor = dev.arena.take<uint32_t>(nb + 1);
-  uint32_t *list = dev.arena.take<uint32_t>((size_t)s.W * n);
   const size_t maxent = (size_t)s.W * n;
-  const size_t nchunks = (maxent + s.CH - 1) / s.CH + 1;
-  uint32_t *heads = dev.arena.take<uint32_t>(nchunks * xw);
-  uint32_t *tails = dev.arena.take<uint32_t>(nchunks * xw);
+  uint32_t *keys = dev.arena.take<uint32_t>(maxent);
+  uint32_t *vals = dev.arena.take<uint32_t>(maxent);
+  uint32_t *skeys = dev.arena.take<uint32_t>(maxent);
+  uint32_t *list = dev.arena.take<uint32_t>(maxent);  // sorted values
+  uint32_t *offsets = dev.arena.take<uint32_t>(nb + 1);
+  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s);
+  uint32_t *ikeys0 = dev.arena.take<uint32_t>(ns0);
+  uint32_t *ivals0 = dev.arena.take<uint32_t>(ns0 * xw);
+  uint32_t *ckeys = dev.arena.take<uint32_t>(ns0);
+  uint32_t *cvals = dev.arena.take<uint32_t>(ns0 * xw);
+  uint32_t *flags = dev.arena.take<uint32_t>(ns0);
+  uint32_t *pos = dev.arena.take<uint32_t>(ns0);
+  uint32_t *ccount = dev.arena.take<uint32_t>(16);
+  uint32_t *okA = dev.arena.take<uint32_t>(ns1);
+  uint32_t *ovA = dev.arena.take<uint32_t>(ns1 * xw);
+  uint32_t *okB = dev.arena.take<uint32_t>(ns1);
+  uint32_t *ovB = dev.arena.take<uint32_t>(ns1 * xw);
   uint32_t *buckets = dev.arena.take<uint32_t>(nb * xw);
   uint32_t *T = dev.arena.take<uint32_t>((size_t)s.W * s.S * xw);
   uint32_t *R = dev.arena.take<uint32_t>((size_t)s.W * s.S * xw);
   uint32_t *P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * s.nchunk * xw);
   uint32_t *P1 = dev.arena.take<uint32_t>((size_t)s.W * s.J * s.nchunk * xw);
   uint64_t *exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
-  size_t cub = 0;
-  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, counts, offsets, (int)(nb + 1), st));
+  size_t cub = 0, cub2 = 0;
+  const int kbits = key_bits(nb);
+  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
+  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
+  if (cub2 > cub) cub = cub2;
   void *cubtmp = dev.arena.take<char>(cub);
 
-  ZK_CHECK(hipMemsetAsync(counts, 0, (nb + 1) * 4, st));
   hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_pt, n, pts_int);
   ZK_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_sc, n, nl, mont ? 1 : 0, c, s.W,
-                     digits, counts);
+                     keys, vals);
   ZK_CHECK(hipGetLastError());
-  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cub, counts, offsets, (int)(nb + 1), st));
-  ZK_CHECK(hipMemcpyAsync(cursor, offsets, (nb + 1) * 4, hipMemcpyDeviceToDevice, st));
-  hipLaunchKernelGGL(k_scatter, dim3(div_up(n, 256)), dim3(256), 0, st, digits, n, c, s.W, cursor, list);
+  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
+  hipLaunchKernelGGL(k_offsets, dim3(div_up(nb + 1, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
+                     (uint32_t)nb, offsets);
   ZK_CHECK(hipGetLastError());
-  uint32_t total = 0;
-  ZK_CHECK(hipMemcpyAsync(&total, offsets + nb, 4, hipMemcpyDeviceToHost, st));
-  ZK_CHECK(hipStreamSynchronize(st));
 
   KernelTimer &kt = dominant_timer();
-  if (total > 0) {
-    const uint32_t nthreads = (total + s.CH - 1) / s.CH;
+  {
     if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev0, st));
-    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(nthreads, 256)), dim3(256), 0, st, pts_int, list, offsets,
-                       (uint32_t)nb, total, s.CH, buckets, heads, tails);
+    // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
+    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(ns0 / 2, 256)), dim3(256), 0, st, pts_int, list, offsets,
+                       (uint32_t)nb, s.CH, buckets, ikeys0, ivals0, (uint32_t)ns0);
     ZK_CHECK(hipGetLastError());
     if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev1, st));
   }
-  hipLaunchKernelGGL(k_fixup<C>, dim3(div_up(nb, 256)), dim3(256), 0, st, offsets, (uint32_t)nb, s.CH, buckets,
-                     heads, tails);
-  ZK_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_seg<C>, dim3(div_up((size_t)s.W * s.S, 256)), dim3(256), 0, st, buckets, s.W, s.B, s.L,
-                     T, R);
+  // stitch levels: compact the partial items, sum them per bucket, repeat
+  {
+    const uint32_t *inK = ikeys0, *inV = ivals0;
+    const uint32_t *inCount = nullptr;  // level 0: every slot is examined
+    size_t slots = ns0;
+    uint32_t *outK = okA, *outV = ovA, *altK = okB, *altV = ovB;
+    for (;;) {
+      hipLaunchKernelGGL(k_item_flags, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, inCount, (uint32_t)slots,
+                         (uint32_t)nb, flags);
+      ZK_CHECK(hipGetLastError());
+      size_t cb = cub;
+      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, flags, pos, (int)slots, st));
+      hipLaunchKernelGGL(k_item_compact<C>, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, inV, flags, pos,
+                         (uint32_t)slots, ckeys, cvals, ccount);
+      ZK_CHECK(hipGetLastError());
+      const bool final_level = slots <= (size_t)s.SCH;  // all items fit one chunk: everything completes
+      const size_t nout = final_level ? 2 : 2 * ((slots + s.SCH - 1) / s.SCH);
+      hipLaunchKernelGGL(k_stitch<C>, dim3(div_up(nout / 2, 256)), dim3(256), 0, st, ckeys, cvals, ccount,
+                         (uint32_t)nb, s.SCH, buckets, outK, outV, (uint32_t)nout);
+      ZK_CHECK(hipGetLastError());
+      if (final_level) break;
+      inK = outK; inV = outV; inCount = nullptr; slots = nout;
+      uint32_t *tk = outK, *tv = outV;
+      outK = altK; outV = altV; altK = tk; altV = tv;
+    }
+  }
+  hipLaunchKernelGGL(k_seg<C>, dim3(div_up((size_t)s.W * s.S, 256)), dim3(256), 0, st, buckets, offsets, s.W, s.B,
+                     s.L, T, R);
   ZK_CHECK(hipGetLastError());
   const int ngrp = s.W * s.J;
   hipLaunchKernelGGL(k_bitsum<C>, dim3(div_up((size_t)ngrp * s.nchunk, 256)), dim3(256), 0, st, T, R, s.W, s.S,
@@ -478,7 +594,7 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(expbytes));
   ZK_CHECK(hipMemcpyAsync(h, exp, expbytes, hipMemcpyDeviceToHost, st));
   ZK_CHECK(hipStreamSynchronize(st));
-  if (kt.enabled && total > 0) {
+  if (kt.enabled) {
     float ms = 0;
     ZK_CHECK(hipEventElapsedTime(&ms, kt.ev0, kt.ev1));
     kt.total_ms += ms;

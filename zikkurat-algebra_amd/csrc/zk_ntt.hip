@@ -8,13 +8,18 @@
 // with canonical outputs, so any correct schedule reproduces them bit for bit.
 //
 // GPU schedule (MI355X-first): N = R_0 * R_1 * ... * R_{P-1}, R_p = 2^r_p <= 256, i.e.
-// P <= 4 HBM passes (3 at 2^24).  Pass p performs, inside LDS, 2^r_p-point DFTs along
-// digit p (stride S_p = R_{p+1}...R_{P-1}) for a tile of G consecutive columns (coalesced
-// 256-B row segments), then multiplies output k_p by the inter-pass twiddle
-// w^(T_p * k_p * lo), T_p = R_0...R_{p-1}, lo = the column index below digit p.  The last
-// pass writes each output straight to its natural index k = sum_q k_q T_q (so no
-// separate bit-reversal pass).  Derivation in DESIGN.md.  Twiddles: w^e for e < N
-// comes from two small tables (w^(e mod 2^h), w^(2^h * (e >> h))), L2-resident.
+// P = ceil(m/8) HBM passes (3 at 2^24); m <= 11 runs as one workgroup-sized pass.
+// Pass p performs, inside LDS, R_p-point DFTs along digit p (stride S_p =
+// R_{p+1}...R_{P-1}) for a tile of G consecutive columns (coalesced 128-B row segments),
+// as radix-4 rounds (two radix-2 DIT stages per LDS round trip), then multiplies output
+// k_p by the inter-pass twiddle w^(T_p * k_p * lo) (T_p = R_0...R_{p-1}, lo = the column
+// below digit p) read from a precomputed per-pass table.  The last pass writes each
+// output straight to its natural index k = sum_q k_q T_q (no bit-reversal pass).
+// Inverse: w -> w^-1 and the 1/N factor folded into pass 0's twiddle table.
+// Twiddle tables are built on the device once per (curve, m, gen, direction) and cached.
+#include <map>
+#include <tuple>
+#include <vector>
 #include "zk_field.hpp"
 #include "zk_host.hpp"
 #include "zk_runtime.hpp"
@@ -22,176 +27,254 @@
 
 namespace zk {
 
-constexpr int NTT_TILE = 2048;  // elements per workgroup tile (R * G)
 constexpr int NTT_THREADS = 256;
+constexpr int NTT_TILE = 1024;  // elements per workgroup tile for multi-pass transforms
 
-struct PassDesc {
-  int r;       // log2 radix of this pass
-  int S;       // stride of digit p, in elements
-  int T;       // product of earlier radices
-  int last;    // 1 for the final pass
-};
+// ---------------------------------------------------------------------------- tables
 
+// w^e from the two-level tables (internal form, stored packed canonical)
 template <class F>
-__device__ __forceinline__ void twiddle(Fe<F> &w, const uint64_t *__restrict__ tlo, const uint64_t *__restrict__ thi,
-                                        int h, uint32_t e) {
-  // tables hold internal-form powers, stored packed (canonical, N64 u64 words)
+__device__ __forceinline__ void tw2(Fe<F> &w, const uint64_t *__restrict__ tlo, const uint64_t *__restrict__ thi,
+                                    int h, uint32_t e) {
   Fe<F> a, b;
   fe_load_ref(a, tlo + (size_t)(e & ((1u << h) - 1)) * F::N64);
   fe_load_ref(b, thi + (size_t)(e >> h) * F::N64);
   fe_mul(w, a, b);
 }
 
+// tlo[i] = w^i (i < 2^h), thi[i] = w^(i 2^h) (i < 2^(m-h)); pows = reference-form w^(2^b)
+template <class F>
+__global__ void k_tw_tables(uint64_t *__restrict__ tlo, uint64_t *__restrict__ thi, int h, int m,
+                            const uint64_t *__restrict__ pows) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nlo = 1 << h, nhi = 1 << (m - h);
+  for (int which = 0; which < 2; which++) {
+    const int cnt = which ? nhi : nlo;
+    if (i >= cnt) continue;
+    const int base = which ? h : 0, nb = which ? m - h : h;
+    Fe<F> acc;
+    fe_one(acc);
+    for (int b = 0; b < nb; b++)
+      if ((i >> b) & 1) {
+        Fe<F> p, q, t;
+        fe_load_ref(q, pows + (size_t)(b + base) * F::N64);
+        fe_to_int(p, q);
+        fe_mul(t, acc, p);
+        acc = t;
+      }
+    fe_store_ref((which ? thi : tlo) + (size_t)i * F::N64, acc);
+  }
+}
+
+// per-pass table: tab[k*S + lo] = w^(T k lo) (* scale, if given), k < R, lo < S
+template <class F>
+__global__ void k_tw_pass(uint64_t *__restrict__ tab, int R, int S, uint32_t T, const uint64_t *__restrict__ tlo,
+                          const uint64_t *__restrict__ thi, int h, const uint64_t *__restrict__ scale) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)R * S) return;
+  const uint32_t k = (uint32_t)(idx / S), lo = (uint32_t)(idx % S);
+  Fe<F> w;
+  tw2(w, tlo, thi, h, T * k * lo);
+  if (scale) {
+    Fe<F> s, t, u;
+    fe_load_ref(s, scale);
+    fe_to_int(t, s);
+    fe_mul(u, w, t);
+    w = u;
+  }
+  fe_store_ref(tab + idx * F::N64, w);
+}
+
+// inner twiddles of an R-point DFT: itw[j] = w_R^j = w^(j N/R), j < R/2
+template <class F>
+__global__ void k_tw_inner(uint64_t *__restrict__ itw, int m, int r, const uint64_t *__restrict__ tlo,
+                           const uint64_t *__restrict__ thi, int h) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (1 << r) / 2) return;
+  Fe<F> w;
+  tw2(w, tlo, thi, h, (uint32_t)j << (m - r));
+  fe_store_ref(itw + (size_t)j * F::N64, w);
+}
+
+// ---------------------------------------------------------------------------- pass kernel
+
+template <class F>
+__device__ __forceinline__ void lds_get(Fe<F> &x, const uint32_t *p) {
+#pragma unroll
+  for (int q = 0; q < F::N; q++) x.v[q] = p[q];
+}
+template <class F>
+__device__ __forceinline__ void lds_put(uint32_t *p, const Fe<F> &x) {
+#pragma unroll
+  for (int q = 0; q < F::N; q++) p[q] = x.v[q];
+}
+
+// in-LDS DIT over G instances of R points (bit-reversed input order -> natural order)
+template <class F>
+__device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int r, int G) {
+  constexpr int NW = F::N;
+  const int R = 1 << r;
+  const int tid = threadIdx.x;
+  int s = 0;
+  for (; s + 1 < r; s += 2) {  // radix-4 rounds: stages s and s+1
+    const int half = 1 << s;
+    const int q4 = R >> 2;
+    for (int u = tid; u < G * q4; u += NTT_THREADS) {
+      const int g = u / q4, j = u % q4;
+      const int blk = j >> s, off = j & (half - 1);
+      const int i0 = g * R + blk * 4 * half + off;
+      Fe<F> a0, a1, a2, a3, w1, w2, w3, t;
+      lds_get(a0, data + (size_t)i0 * NW);
+      lds_get(a1, data + (size_t)(i0 + half) * NW);
+      lds_get(a2, data + (size_t)(i0 + 2 * half) * NW);
+      lds_get(a3, data + (size_t)(i0 + 3 * half) * NW);
+      lds_get(w1, itw + (size_t)(off * (R / (2 * half))) * NW);           // w_{2h}^off
+      lds_get(w2, itw + (size_t)(off * (R / (4 * half))) * NW);           // w_{4h}^off
+      lds_get(w3, itw + (size_t)((off + half) * (R / (4 * half))) * NW);  // w_{4h}^(off+h)
+      // stage s
+      Fe<F> b0, b1, b2, b3;
+      fe_mul(t, a1, w1);
+      fe_add(b0, a0, t);
+      fe_sub(b1, a0, t);
+      fe_mul(t, a3, w1);
+      fe_add(b2, a2, t);
+      fe_sub(b3, a2, t);
+      // stage s+1
+      fe_mul(t, b2, w2);
+      fe_add(a0, b0, t);
+      fe_sub(a2, b0, t);
+      fe_mul(t, b3, w3);
+      fe_add(a1, b1, t);
+      fe_sub(a3, b1, t);
+      lds_put(data + (size_t)i0 * NW, a0);
+      lds_put(data + (size_t)(i0 + half) * NW, a1);
+      lds_put(data + (size_t)(i0 + 2 * half) * NW, a2);
+      lds_put(data + (size_t)(i0 + 3 * half) * NW, a3);
+    }
+    __syncthreads();
+  }
+  if (s < r) {  // odd r: one radix-2 stage left
+    const int half = 1 << s;
+    const int q2 = R >> 1;
+    for (int u = tid; u < G * q2; u += NTT_THREADS) {
+      const int g = u / q2, j = u % q2;
+      const int blk = j >> s, off = j & (half - 1);
+      const int i0 = g * R + blk * 2 * half + off;
+      Fe<F> a, b, w, t, x, y;
+      lds_get(a, data + (size_t)i0 * NW);
+      lds_get(b, data + (size_t)(i0 + half) * NW);
+      lds_get(w, itw + (size_t)(off * (R / (2 * half))) * NW);
+      fe_mul(t, b, w);
+      fe_add(x, a, t);
+      fe_sub(y, a, t);
+      lds_put(data + (size_t)i0 * NW, x);
+      lds_put(data + (size_t)(i0 + half) * NW, y);
+    }
+    __syncthreads();
+  }
+}
+
+struct PassArgs {
+  int m, r, S, T, last, G, P;
+  int dig[8];  // log2 radix of every pass
+};
+
 // One pass.  Block = one tile of G instances x R elements.
-//   non-last pass: instance (hi, lo) with lo in [0, S); element k at hi*R*S + k*S + lo
-//                  tile = G consecutive lo for one hi
-//   last pass    : S == 1; instance = position prefix; element k at inst*R + k;
-//                  tile = G instances with consecutive digit k_0 (stride S_0/R in inst)
-//                  output to natural index natbase(inst) + k * T
+//   non-last pass: instance (hi, lo), lo in [0, S); element k at hi*R*S + k*S + lo
+//                  tile = G consecutive lo for one hi; output * tab[k*S + lo]
+//   last pass    : S == 1; instance = position prefix (k_0..k_{P-2}); element k at inst*R + k;
+//                  tile = G instances with consecutive k_0; output to natural index
 template <class F>
 __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__restrict__ src, uint64_t *__restrict__ dst,
-                                                          int m, int r, int S, int T, int last, int G,
-                                                          const int *__restrict__ digits_r, int P,
-                                                          const uint64_t *__restrict__ tlo,
-                                                          const uint64_t *__restrict__ thi, int h,
+                                                          PassArgs a, const uint64_t *__restrict__ itw_g,
+                                                          const uint64_t *__restrict__ tab,
                                                           const uint64_t *__restrict__ scale) {
   extern __shared__ uint32_t lds[];
-  constexpr int NW = F::N;  // u32 words per element
+  constexpr int NW = F::N;
+  const int r = a.r, G = a.G, S = a.S;
   const int R = 1 << r;
-  const int halfR = R >> 1;
   uint32_t *data = lds;                          // [G][R] elements
-  uint32_t *itw = lds + (size_t)G * R * NW;      // [R/2] inner twiddles w_R^j
+  uint32_t *itw = lds + (size_t)G * R * NW;      // [R/2] inner twiddles
   const int tid = threadIdx.x;
-  const uint32_t N = 1u << m;
+  const int tile = blockIdx.x;
 
-  // inner twiddles: w_R^j = w_N^(j * N/R)
-  for (int j = tid; j < halfR; j += NTT_THREADS) {
+  for (int j = tid; j < R / 2; j += NTT_THREADS) {
     Fe<F> w;
-    twiddle(w, tlo, thi, h, (uint32_t)j * (N >> r));
-#pragma unroll
-    for (int q = 0; q < NW; q++) itw[j * NW + q] = w.v[q];
+    fe_load_ref(w, itw_g + (size_t)j * F::N64);
+    lds_put(itw + (size_t)j * NW, w);
   }
 
-  // tile -> instance mapping
-  const int tile = blockIdx.x;
-  size_t in_base[1];  // silence unused warnings on some compilers
-  (void)in_base;
+  // instance geometry of this tile
+  size_t hi_base = 0;  // non-last: hi * R * S + lo0
+  size_t pos_base = 0, nat_base = 0;  // last: position / natural index of instance k_0 = k0base
+  int k0base = 0, k0stride_pos = 0;
+  if (!a.last) {
+    const int ntl = S / G;
+    hi_base = (size_t)(tile / ntl) * R * S + (size_t)(tile % ntl) * G;
+  } else if (a.P > 1) {
+    const int R0 = 1 << a.dig[0];
+    const int ntile0 = R0 / G;
+    k0base = (tile % ntile0) * G;
+    int rem = tile / ntile0;
+    size_t Sq = (size_t)1 << a.m;
+    size_t Tq = (size_t)R0;
+    for (int q = 0; q < a.P - 1; q++) {
+      Sq >>= a.dig[q];
+      if (q == 0) {
+        k0stride_pos = (int)(Sq >> r);  // position stride of k_0, in units of R
+      } else {
+        const int kq = rem & ((1 << a.dig[q]) - 1);
+        rem >>= a.dig[q];
+        pos_base += (size_t)kq * Sq;
+        nat_base += (size_t)kq * Tq;
+        Tq <<= a.dig[q];
+      }
+    }
+  }
 
-  // load: element (g, k) -> LDS slot g*R + bitrev(k)
+  // load: element (g, k) -> LDS slot g*R + bitrev_r(k)
   const int nel = G * R;
   for (int e = tid; e < nel; e += NTT_THREADS) {
     int g, k;
     size_t addr;
-    if (!last) {
+    if (!a.last) {
       g = e % G;
       k = e / G;
-      const int ntile_lo = S / G;  // S multiple of G
-      const int hi = tile / ntile_lo;
-      const int lo = (tile % ntile_lo) * G + g;
-      addr = (size_t)hi * R * S + (size_t)k * S + lo;
+      addr = hi_base + (size_t)k * S + g;
     } else {
       g = e / R;
       k = e % R;
-      // instance index: digits (k_0, ..., k_{P-2}); tile covers G consecutive k_0
-      const int R0 = 1 << digits_r[0];
-      const int ntile0 = R0 / G;
-      const int k0 = (tile % ntile0) * G + g;
-      const int rest = tile / ntile0;  // enumerates k_1..k_{P-2}
-      // position prefix (in units of R_last): k_0 * S_0/R + sum_{1<=q<P-1} k_q * S_q/R
-      size_t pos = 0;
-      int rem = rest;
-      size_t Sq = (size_t)N;  // S_q * R_q running
-      for (int q = 0; q < P - 1; q++) {
-        Sq >>= digits_r[q];
-        int kq;
-        if (q == 0) kq = k0;
-        else { kq = rem & ((1 << digits_r[q]) - 1); rem >>= digits_r[q]; }
-        pos += (size_t)kq * Sq;
-      }
-      addr = pos + k;
+      addr = pos_base + ((size_t)(k0base + g) * k0stride_pos) * R + k;
+      if (a.P == 1) addr = k;
     }
     Fe<F> x;
     fe_load_ref(x, src + addr * F::N64);
     const int kr = r ? (int)(__builtin_bitreverse32((uint32_t)k) >> (32 - r)) : 0;
-    uint32_t *d = data + ((size_t)g * R + kr) * NW;
-#pragma unroll
-    for (int q = 0; q < NW; q++) d[q] = x.v[q];
+    lds_put(data + ((size_t)g * R + kr) * NW, x);
   }
   __syncthreads();
 
-  // radix-2 DIT stages in LDS
-  for (int s = 0; s < r; s++) {
-    const int half = 1 << s;
-    const int tstep = halfR >> s;  // w_{2half}^j = w_R^(j * R/(2 half))
-    for (int bf = tid; bf < G * halfR; bf += NTT_THREADS) {
-      const int g = bf / halfR;
-      const int j = bf % halfR;
-      const int blk = j >> s;
-      const int off = j & (half - 1);
-      const int i0 = g * R + blk * 2 * half + off;
-      const int i1 = i0 + half;
-      Fe<F> a, b, w, t;
-#pragma unroll
-      for (int q = 0; q < NW; q++) {
-        a.v[q] = data[i0 * NW + q];
-        b.v[q] = data[i1 * NW + q];
-        w.v[q] = itw[(off * tstep) * NW + q];
-      }
-      fe_mul(t, b, w);
-      Fe<F> u, v;
-      fe_add(u, a, t);
-      fe_sub(v, a, t);
-#pragma unroll
-      for (int q = 0; q < NW; q++) {
-        data[i0 * NW + q] = u.v[q];
-        data[i1 * NW + q] = v.v[q];
-      }
-    }
-    __syncthreads();
-  }
+  lds_dft<F>(data, itw, r, G);
 
-  // store (with inter-pass twiddle, or to natural positions on the last pass)
   Fe<F> sc;
-  if (last && scale) {
+  if (scale) {
     Fe<F> t;
     fe_load_ref(t, scale);
     fe_to_int(sc, t);
   }
   for (int e = tid; e < nel; e += NTT_THREADS) {
-    int g = e % G, k = e / G;  // consecutive threads -> consecutive g (coalesced)
+    const int g = e % G, k = e / G;  // consecutive threads -> consecutive g (coalesced)
     Fe<F> x;
-    const uint32_t *d = data + ((size_t)g * R + k) * NW;
-#pragma unroll
-    for (int q = 0; q < NW; q++) x.v[q] = d[q];
+    lds_get(x, data + ((size_t)g * R + k) * NW);
     size_t addr;
-    if (!last) {
-      const int ntile_lo = S / G;
-      const int hi = tile / ntile_lo;
-      const int lo = (tile % ntile_lo) * G + g;
-      addr = (size_t)hi * R * S + (size_t)k * S + lo;
-      if (lo != 0 && k != 0) {
-        Fe<F> w, y;
-        twiddle(w, tlo, thi, h, (uint32_t)((size_t)T * k * lo));
-        fe_mul(y, x, w);
-        x = y;
-      }
+    if (!a.last) {
+      addr = hi_base + (size_t)k * S + g;
+      Fe<F> w, y;
+      fe_load_ref(w, tab + ((size_t)k * S + (addr % S)) * F::N64);
+      fe_mul(y, x, w);
+      x = y;
     } else {
-      const int R0 = 1 << digits_r[0];
-      const int ntile0 = R0 / G;
-      const int k0 = (tile % ntile0) * G + g;
-      const int rest = tile / ntile0;
-      // natural index: k_0 + sum_{1<=q<P-1} k_q T_q + k * T_last
-      size_t nat = (size_t)k0;
-      int rem = rest;
-      size_t Tq = (size_t)R0;
-      for (int q = 1; q < P - 1; q++) {
-        int kq = rem & ((1 << digits_r[q]) - 1);
-        rem >>= digits_r[q];
-        nat += (size_t)kq * Tq;
-        Tq <<= digits_r[q];
-      }
-      addr = nat + (size_t)k * T;
-      if (P == 1) addr = k;
+      addr = (a.P == 1) ? (size_t)k : nat_base + (size_t)(k0base + g) + (size_t)k * a.T;
       if (scale) {
         Fe<F> y;
         fe_mul(y, x, sc);
@@ -202,42 +285,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
   }
 }
 
-// twiddle tables: tlo[i] = w^i (i < 2^h), thi[i] = w^(i * 2^h) (i < 2^(m-h))
-template <class F>
-__global__ void k_tw_tables(uint64_t *__restrict__ tlo, uint64_t *__restrict__ thi, int h, int m,
-                            const uint64_t *__restrict__ pows /* w^(2^b), b < m */) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nlo = 1 << h, nhi = 1 << (m - h);
-  if (i < nlo) {
-    Fe<F> acc;
-    fe_one(acc);
-    for (int b = 0; b < h; b++)
-      if ((i >> b) & 1) {
-        Fe<F> p, q, t;
-        fe_load_ref(q, pows + (size_t)b * F::N64);
-        fe_to_int(p, q);
-        fe_mul(t, acc, p);
-        acc = t;
-      }
-    fe_store_ref(tlo + (size_t)i * F::N64, acc);
-  }
-  if (i < nhi) {
-    Fe<F> acc;
-    fe_one(acc);
-    for (int b = 0; b < m - h; b++)
-      if ((i >> b) & 1) {
-        Fe<F> p, q, t;
-        fe_load_ref(q, pows + (size_t)(b + h) * F::N64);
-        fe_to_int(p, q);
-        fe_mul(t, acc, p);
-        acc = t;
-      }
-    fe_store_ref(thi + (size_t)i * F::N64, acc);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// host side
+// ---------------------------------------------------------------------------- host side
 
 static void split_digits(int m, std::vector<int> &d) {
   d.clear();
@@ -248,19 +296,42 @@ static void split_digits(int m, std::vector<int> &d) {
   for (int p = 0; p < P; p++) d.push_back(base + (p < extra ? 1 : 0));
 }
 
-template <class Cfg>
-static void ntt_run(Device &dev, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst,
-                    bool host_io, bool inverse) {
-  using F = typename Cfg::Fd;   // device field
-  using HF = typename Cfg::Fh;  // host field
-  const size_t N = (size_t)1 << m;
-  hipStream_t st = dev.stream;
+// cached twiddle set for one (curve, m, gen, direction)
+struct TwSet {
+  uint64_t *mem = nullptr;       // one allocation
+  std::vector<uint64_t *> inner; // per pass: R_p/2 inner twiddles
+  std::vector<uint64_t *> tab;   // per non-last pass: R_p * S_p table
+  uint64_t *scale = nullptr;     // 1/N (reference form) for the single-pass inverse
+  size_t bytes = 0;
+  uint64_t last_use = 0;
+};
+typedef std::tuple<int, int, int, uint64_t, uint64_t, uint64_t, uint64_t> TwKey;
+static std::map<TwKey, TwSet> g_tw;  // entries of device d are only touched under d's mutex
+static std::mutex g_tw_mu;          // guards the map structure itself
+static uint64_t g_tw_clock = 0;
+static const size_t TW_CACHE_LIMIT = (size_t)8 << 30;
 
-  // host: w (forward) or w^-1 (inverse), its 2^b powers, and 1/N
+template <class Cfg>
+static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, bool inverse,
+                       const std::vector<int> &dig) {
+  using F = typename Cfg::Fd;
+  using HF = typename Cfg::Fh;
+  TwKey key(dev.id * 2 + curve, m, inverse, gen_mont[0], gen_mont[1], gen_mont[2], gen_mont[3]);
+  std::lock_guard<std::mutex> lock(g_tw_mu);
+  auto it = g_tw.find(key);
+  if (it != g_tw.end()) {
+    it->second.last_use = ++g_tw_clock;
+    return it->second;
+  }
+  const size_t N = (size_t)1 << m;
+  const int P = (int)dig.size();
+  const int h = m / 2;
+  const size_t el = F::N64;
+  // host: w (or w^-1), its 2^b powers, 1/N
   zkh::Fe<HF> g;
   memcpy(g.v, gen_mont, sizeof g.v);
   if (inverse) zkh::inv(g, g);
-  std::vector<uint64_t> pows((size_t)(m > 0 ? m : 1) * HF::N);
+  std::vector<uint64_t> pows((size_t)(m > 0 ? m : 1) * HF::N, 0);
   {
     zkh::Fe<HF> p = g;
     for (int b = 0; b < m; b++) {
@@ -272,30 +343,101 @@ static void ntt_run(Device &dev, int m, const uint64_t *gen_mont, const uint64_t
   {
     zkh::Fe<HF> nn;
     zkh::set_zero(nn);
-    // N in standard form -> Montgomery -> inverse
-    if (m < 64) nn.v[0] = (uint64_t)1 << m;
+    nn.v[0] = (uint64_t)1 << m;
     zkh::to_mont(nn, nn);
     zkh::inv(ninv, nn);
   }
+  // sizes
+  size_t words = ((size_t)1 << h) * el + ((size_t)1 << (m - h)) * el + pows.size() + 2 * el;
+  size_t S = N, T = 1;
+  std::vector<size_t> tab_words(P, 0);
+  for (int p = 0; p < P; p++) {
+    S >>= dig[p];
+    words += ((size_t)1 << dig[p]) / 2 * el + el;
+    if (p < P - 1) { tab_words[p] = ((size_t)1 << dig[p]) * S * el; words += tab_words[p]; }
+    T <<= dig[p];
+  }
+  // evict least-recently used sets beyond the cache limit
+  size_t total = words * 8;
+  for (auto &kv : g_tw)
+    if (std::get<0>(kv.first) / 2 == dev.id) total += kv.second.bytes;
+  while (total > TW_CACHE_LIMIT) {
+    auto victim = g_tw.end();
+    for (auto i2 = g_tw.begin(); i2 != g_tw.end(); ++i2)
+      if (std::get<0>(i2->first) / 2 == dev.id &&
+          (victim == g_tw.end() || i2->second.last_use < victim->second.last_use))
+        victim = i2;
+    if (victim == g_tw.end()) break;
+    total -= victim->second.bytes;
+    ZK_CHECK(hipStreamSynchronize(dev.stream));
+    ZK_CHECK(hipFree(victim->second.mem));
+    g_tw.erase(victim);
+  }
+  TwSet ts;
+  ts.bytes = words * 8;
+  ZK_CHECK(hipMalloc(&ts.mem, ts.bytes));
+  uint64_t *cur = ts.mem;
+  auto take = [&](size_t w) { uint64_t *p = cur; cur += (w + 1) & ~size_t(1); return p; };
+  uint64_t *tlo = take(((size_t)1 << h) * el);
+  uint64_t *thi = take(((size_t)1 << (m - h)) * el);
+  uint64_t *d_pows = take(pows.size());
+  uint64_t *d_ninv = take(el);
+  hipStream_t st = dev.stream;
+  ZK_CHECK(hipMemcpyAsync(d_pows, pows.data(), pows.size() * 8, hipMemcpyHostToDevice, st));
+  ZK_CHECK(hipMemcpyAsync(d_ninv, ninv.v, el * 8, hipMemcpyHostToDevice, st));
+  {
+    const int nt = 1 << (h > m - h ? h : m - h);
+    hipLaunchKernelGGL(k_tw_tables<F>, dim3(div_up(nt, 256)), dim3(256), 0, st, tlo, thi, h, m, d_pows);
+    ZK_CHECK(hipGetLastError());
+  }
+  S = N;
+  T = 1;
+  for (int p = 0; p < P; p++) {
+    const int r = dig[p];
+    S >>= r;
+    uint64_t *inner = take(((size_t)1 << r) / 2 * el + el);
+    if (r > 0) {
+      hipLaunchKernelGGL(k_tw_inner<F>, dim3(div_up(((size_t)1 << r) / 2, 256)), dim3(256), 0, st, inner, m, r, tlo,
+                         thi, h);
+      ZK_CHECK(hipGetLastError());
+    }
+    ts.inner.push_back(inner);
+    if (p < P - 1) {
+      uint64_t *tab = take(tab_words[p]);
+      const size_t cnt = ((size_t)1 << r) * S;
+      hipLaunchKernelGGL(k_tw_pass<F>, dim3(div_up(cnt, 256)), dim3(256), 0, st, tab, 1 << r, (int)S, (uint32_t)T,
+                         tlo, thi, h, (inverse && p == 0) ? d_ninv : nullptr);
+      ZK_CHECK(hipGetLastError());
+      ts.tab.push_back(tab);
+    } else {
+      ts.tab.push_back(nullptr);
+    }
+    T <<= r;
+  }
+  ts.scale = (inverse && P == 1) ? d_ninv : nullptr;
+  ts.last_use = ++g_tw_clock;
+  return g_tw.emplace(key, ts).first->second;
+}
 
+struct CfgBN { using Fd = BN_Fr; using Fh = zkh::BN_Fr; };
+struct CfgBLS { using Fd = BLS_Fr; using Fh = zkh::BLS_Fr; };
+
+template <class Cfg>
+static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst,
+                    bool host_io, bool inverse) {
+  using F = typename Cfg::Fd;
+  const size_t N = (size_t)1 << m;
+  hipStream_t st = dev.stream;
   std::vector<int> dig;
   split_digits(m, dig);
   const int P = (int)dig.size();
-  const int h = m / 2;
+  TwSet &tw = twiddles<Cfg>(dev, curve, m, gen_mont, inverse, dig);
 
   const size_t elbytes = (size_t)F::N64 * 8;
-  size_t need = 0;
-  auto acc = [&](size_t b) { need += (b + 255) & ~size_t(255); };
-  if (host_io) { acc(N * elbytes); acc(N * elbytes); }
-  acc(N * elbytes);                              // scratch
-  acc(((size_t)1 << h) * elbytes);
-  acc(((size_t)1 << (m - h)) * elbytes);
-  acc(pows.size() * 8);
-  acc(elbytes);
-  acc(64 * sizeof(int));
-  dev.arena.reserve(need + (1 << 20));
+  size_t need = N * elbytes + (1 << 20);
+  if (host_io) need += 2 * N * elbytes;
+  dev.arena.reserve(need);
   dev.arena.reset();
-
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
   if (host_io) {
@@ -305,25 +447,14 @@ static void ntt_run(Device &dev, int m, const uint64_t *gen_mont, const uint64_t
     d_dst = dev.arena.take<uint64_t>(N * F::N64);
   }
   uint64_t *scratch = dev.arena.take<uint64_t>(N * F::N64);
-  uint64_t *tlo = dev.arena.take<uint64_t>(((size_t)1 << h) * F::N64);
-  uint64_t *thi = dev.arena.take<uint64_t>(((size_t)1 << (m - h)) * F::N64);
-  uint64_t *d_pows = dev.arena.take<uint64_t>(pows.size());
-  uint64_t *d_scale = dev.arena.take<uint64_t>(F::N64);
-  int *d_dig = dev.arena.take<int>(64);
-  ZK_CHECK(hipMemcpyAsync(d_pows, pows.data(), pows.size() * 8, hipMemcpyHostToDevice, st));
-  ZK_CHECK(hipMemcpyAsync(d_scale, ninv.v, elbytes, hipMemcpyHostToDevice, st));
-  ZK_CHECK(hipMemcpyAsync(d_dig, dig.data(), dig.size() * sizeof(int), hipMemcpyHostToDevice, st));
-  {
-    const int nt = 1 << (h > m - h ? h : m - h);
-    hipLaunchKernelGGL(k_tw_tables<F>, dim3(div_up(nt, 256)), dim3(256), 0, st, tlo, thi, h, m, d_pows);
-    ZK_CHECK(hipGetLastError());
-  }
 
-  // pass chain: src -> scratch -> (in place) ... -> dst
   KernelTimer &kt = dominant_timer();
-  size_t S = N;
-  size_t T = 1;
+  size_t S = N, T = 1;
   const uint64_t *in = d_src;
+  PassArgs pa;
+  pa.m = m;
+  pa.P = P;
+  for (int p = 0; p < P && p < 8; p++) pa.dig[p] = dig[p];
   for (int p = 0; p < P; p++) {
     const int r = dig[p];
     const int R = 1 << r;
@@ -331,22 +462,26 @@ static void ntt_run(Device &dev, int m, const uint64_t *gen_mont, const uint64_t
     const int last = (p == P - 1);
     uint64_t *out = last ? d_dst : scratch;
     int G;
-    size_t ntiles;
-    if (!last) {
+    if (P == 1) {
+      G = 1;
+    } else if (!last) {
       G = NTT_TILE / R;
       if ((size_t)G > S) G = (int)S;
-      ntiles = N / ((size_t)R * G);
     } else {
-      const int R0 = 1 << dig[0];
-      G = (P == 1) ? 1 : NTT_TILE / R;
-      if (G > R0) G = R0;
-      if (P == 1) G = 1;
-      ntiles = N / ((size_t)R * G);
+      G = NTT_TILE / R;
+      if (G > (1 << dig[0])) G = 1 << dig[0];
     }
+    const size_t ntiles = N / ((size_t)R * G);
     const size_t lds = ((size_t)G * R + R / 2) * F::N * 4;
+    pa.r = r;
+    pa.S = (int)S;
+    pa.T = (int)T;
+    pa.last = last;
+    pa.G = G;
+    ZK_CHECK(hipFuncSetAttribute((const void *)k_ntt_pass<F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (kt.enabled && p == 0) ZK_CHECK(hipEventRecord(kt.ev0, st));
-    hipLaunchKernelGGL(k_ntt_pass<F>, dim3((unsigned)ntiles), dim3(NTT_THREADS), lds, st, in, out, m, r, (int)S,
-                       (int)T, last, G, d_dig, P, tlo, thi, h, (last && inverse) ? d_scale : nullptr);
+    hipLaunchKernelGGL(k_ntt_pass<F>, dim3((unsigned)ntiles), dim3(NTT_THREADS), lds, st, in, out, pa, tw.inner[p],
+                       tw.tab[p], last ? tw.scale : nullptr);
     ZK_CHECK(hipGetLastError());
     if (kt.enabled && last) ZK_CHECK(hipEventRecord(kt.ev1, st));
     in = out;
@@ -362,16 +497,13 @@ static void ntt_run(Device &dev, int m, const uint64_t *gen_mont, const uint64_t
   }
 }
 
-struct CfgBN { using Fd = BN_Fr; using Fh = zkh::BN_Fr; };
-struct CfgBLS { using Fd = BLS_Fr; using Fh = zkh::BLS_Fr; };
-
 void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst, bool host_io,
          bool inverse) {
   ZK_REQUIRE(m >= 0 && m <= 30, "ntt: log2 size out of range (0..30)");
   Device &dev = current_device();
   std::lock_guard<std::mutex> lock(dev.mu);
-  if (curve == 0) ntt_run<CfgBN>(dev, m, gen_mont, src, dst, host_io, inverse);
-  else ntt_run<CfgBLS>(dev, m, gen_mont, src, dst, host_io, inverse);
+  if (curve == 0) ntt_run<CfgBN>(dev, curve, m, gen_mont, src, dst, host_io, inverse);
+  else ntt_run<CfgBLS>(dev, curve, m, gen_mont, src, dst, host_io, inverse);
 }
 
 }  // namespace zk

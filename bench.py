@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-ntt", action="store_true")
     ap.add_argument("--cpu-sample-log", type=int, default=18, help="log2 pairs in the bounded CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for the partial-sum exchange (nccl = RCCL over xGMI)")
     return ap.parse_args()
 
 
@@ -84,13 +86,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    zk.require_gpu()
+    device = local % zk.device_count()  # (several ranks share a GPU only in single-GPU rehearsals)
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    zk.require_gpu()
-    zk.load().zkg_set_device(local)
+        if args.backend == "nccl":
+            torch.cuda.set_device(device)
+        dist.init_process_group(args.backend)
+    zk.load().zkg_set_device(device)
+    xdev = "cuda" if args.backend == "nccl" else None
 
     curve = args.curve
     n_local = 1 << args.log_n
@@ -106,7 +111,7 @@ def main():
     def step():
         partial = zk.msm_device(curve, n_local, d_s, d_p, mont=True, window=args.window)
         if world > 1:
-            parts = allgather_partials(partial, device="cuda")
+            parts = allgather_partials(partial, device=xdev)
             _, aff = combine_partials(curve, parts)
         else:
             aff = zk.g1_to_affine(curve, partial)
@@ -129,7 +134,7 @@ def main():
     kt_ms, kt_n = zk.timer(enable=False)
     if world > 1:
         import torch
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64, device=xdev or "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
@@ -141,6 +146,7 @@ def main():
     achieved = algo_bytes / accum_s / 1e9
     madds = windows_used(c) * n_local
     pmc = load_pmc("k_accum")
+    mul_peak = zk.field_mul_rate(curve, "fp")
 
     # parity of the timed result against the reference's own output (tests/golden)
     parity = None
@@ -175,8 +181,11 @@ def main():
                      "kernel_ms": accum_s * 1e3,
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "note": "MSM is VALU integer-multiply bound; see valu_roofline"},
-        "valu_roofline": {"madds_per_launch": madds, "fp_muls_per_launch": 10 * madds,
-                          "achieved_fp_muls_per_s": 10 * madds / accum_s},
+        "valu_roofline": {"bound": "valu (v_mad_u64_u32)", "madds_per_launch": madds,
+                          "fp_muls_per_launch": 10 * madds, "unit": "Fp products/s",
+                          "achieved": 10 * madds / accum_s, "peak": mul_peak,
+                          "frac": 10 * madds / accum_s / mul_peak,
+                          "peak_source": "zkg_field_mul_rate: live probe of the same fe_mul on this GPU"},
         "input_gen_s": gen_s,
     }
 
@@ -207,6 +216,7 @@ def bench_ntt(zk, args):
     zk.ntt_device(curve, m, g, d_f, d_i, inverse=True)
     zk.load().zkg_device_synchronize()
     res = {}
+    fr_peak = zk.field_mul_rate(curve, "fr")
     for name, src, dst, inv in (("forward", d_x, d_f, False), ("inverse", d_f, d_i, True)):
         zk.timer(enable=True, reset=True)
         t0 = time.perf_counter()
@@ -216,7 +226,10 @@ def bench_ntt(zk, args):
         dt = (time.perf_counter() - t0) / args.ntt_steps
         kms, kn = zk.timer(enable=False)
         kt = kms / kn / 1e3
+        muls = n // 2 * m + 2 * n  # butterfly products + two inter-pass twiddle products per element
         res[name] = {"elems_per_s": n / dt, "ms": dt * 1e3, "kernel_ms": kt * 1e3,
+                     "valu_roofline": {"fr_muls": muls, "achieved": muls / kt, "peak": fr_peak,
+                                       "frac": muls / kt / fr_peak, "unit": "Fr products/s"},
                      "roofline": {"bound": "hbm", "achieved": NTT_BYTES_PER_ELEM * n / kt / 1e9,
                                   "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                   "frac": NTT_BYTES_PER_ELEM * n / kt / 1e9 / HBM_PEAK_GBPS}}

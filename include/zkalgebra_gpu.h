@@ -112,6 +112,10 @@ ZKG_API void zkg_gen_g1_points(int curve, uint64_t seed, int64_t start, int64_t 
  * (Class/FFT.hs:60-66; BLS12_381/Fr/Mont.hs:145-151, BN128/Fr/Mont.hs:146-148) */
 ZKG_API void zkg_fft_generator(int curve, int m, uint64_t *out);
 
+/* live VALU roofline probe: Montgomery products per second of the device field engine;
+ * field: 0 = bn128 Fp, 1 = bn128 Fr, 2 = bls12_381 Fp, 3 = bls12_381 Fr */
+ZKG_API double zkg_field_mul_rate(int field);
+
 /* MSM window heuristic used when window_size is not given */
 ZKG_API int zkg_msm_default_window(int npoints);
 

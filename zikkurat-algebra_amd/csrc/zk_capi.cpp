@@ -15,6 +15,7 @@
 #include "zk_ntt.hpp"
 #include "zk_runtime.hpp"
 
+namespace zk { double field_mul_rate(int field); }  // zk_probe.hip
 using namespace zk;
 
 namespace {
@@ -229,6 +230,8 @@ ZKG_API void zkg_fft_generator(int curve, int m, uint64_t *out) {
 }
 
 ZKG_API int zkg_msm_default_window(int npoints) { return zk::msm_default_window(npoints); }
+
+ZKG_API double zkg_field_mul_rate(int field) { return zk::field_mul_rate(field); }
 
 ZKG_API void zkg_timer_enable(int on) {
   KernelTimer &t = dominant_timer();

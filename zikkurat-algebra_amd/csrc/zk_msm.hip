@@ -18,9 +18,9 @@
 //                   balanced scheme, level after level (log_{SCH/2} levels): no serial
 //                   loop anywhere, so skewed scalars (all equal, carry windows) stay fast
 //   6. k_seg        per (window, segment of L buckets): T = sum B_m, R = sum (m-lo+1) B_m
-//   7. k_bitsum     sum_m m B_m = sum_s R_s + L * sum_k 2^k U_k, U_k = sum_{s: bit k} T_s:
-//                   every term is a plain point sum -> wide, shallow reductions
-//   8. k_sumseg     further plain-sum levels until one point per (window, job)
+//   7. k_jobsum     sum_m m B_m = sum_s R_s + L * sum_k 2^k U_k, U_k = sum_{s: bit k} T_s:
+//                   every term is a plain point sum; one workgroup per (window, job)
+//                   with an LDS tree
 //   9. host         Horner over the power-of-two exponents, normalise / to_affine
 //
 // Every phase is wide (>= ~1e5 threads at 2^20) except the last tiny levels: a lone
@@ -312,24 +312,22 @@ __global__ void __launch_bounds__(256) k_seg(const uint32_t *__restrict__ bucket
   xyzz_store(Rout + (size_t)g * xyzz_words<F>(), R);
 }
 
-// 7. job j < logS: partial sums of T_s over s with bit j set; job logS: partial sums of R_s.
-//    thread per (window, job, chunk)
+// 7. one workgroup per (window, job): job j < logS sums U_j = sum_{s: bit j of s} T_s,
+//    job logS sums R_s.  Each thread first adds a strided share of the job's items, then
+//    the workgroup folds the partials with an LDS tree: serial depth ~ items/JT + log2(JT)
+//    point adds (the narrow tail of the reduction is latency bound on CDNA4).
+constexpr int JT = 256;
 template <class C>
-__global__ void __launch_bounds__(256) k_bitsum(const uint32_t *__restrict__ T, const uint32_t *__restrict__ R,
-                                                int W, int S, int logS, int CH2, int nchunk,
-                                                uint32_t *__restrict__ out) {
+__global__ void __launch_bounds__(JT) k_jobsum(const uint32_t *__restrict__ T, const uint32_t *__restrict__ R,
+                                              int S, int logS, uint32_t *__restrict__ out) {
   using F = typename C::Fp;
+  extern __shared__ uint32_t lds[];
   const int J = logS + 1;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= W * J * nchunk) return;
-  const int ch = g % nchunk;
-  const int j = (g / nchunk) % J;
-  const int w = g / (nchunk * J);
+  const int w = blockIdx.x / J, j = blockIdx.x % J;
   const int n = (j < logS) ? (S >> 1) : S;
   Xyzz<F> acc;
   xyzz_set_inf(acc);
-  const int e0 = ch * CH2, e1 = min(n, e0 + CH2);
-  for (int e = e0; e < e1; e++) {
+  for (int e = threadIdx.x; e < n; e += JT) {
     Xyzz<F> p;
     if (j < logS) {
       const int lowmask = (1 << j) - 1;
@@ -340,27 +338,21 @@ __global__ void __launch_bounds__(256) k_bitsum(const uint32_t *__restrict__ T, 
     }
     xyzz_add(acc, p);
   }
-  xyzz_store(out + (size_t)g * xyzz_words<F>(), acc);
-}
-
-// 8. plain segmented sum: in[grp][n] -> out[grp][ceil(n/G)]
-template <class C>
-__global__ void __launch_bounds__(256) k_sumseg(const uint32_t *__restrict__ in, int ngrp, int n, int G,
-                                                uint32_t *__restrict__ out) {
-  using F = typename C::Fp;
-  const int nout = (n + G - 1) / G;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ngrp * nout) return;
-  const int grp = g / nout, o = g % nout;
-  Xyzz<F> acc;
-  xyzz_set_inf(acc);
-  const int e1 = min(n, (o + 1) * G);
-  for (int e = o * G; e < e1; e++) {
-    Xyzz<F> p;
-    xyzz_load(p, in + ((size_t)grp * n + e) * xyzz_words<F>());
-    xyzz_add(acc, p);
+  int active = min(JT, n);
+  for (int stride = JT / 2; stride >= 1; stride >>= 1) {
+    if (stride >= active) continue;  // uniform across the block
+    if (threadIdx.x >= stride && threadIdx.x < 2 * stride && threadIdx.x < active)
+      xyzz_store(lds + (size_t)(threadIdx.x - stride) * xyzz_words<F>(), acc);
+    __syncthreads();
+    if (threadIdx.x < stride && threadIdx.x + stride < active) {
+      Xyzz<F> p;
+      xyzz_load(p, lds + (size_t)threadIdx.x * xyzz_words<F>());
+      xyzz_add(acc, p);
+    }
+    __syncthreads();
+    active = stride;
   }
-  xyzz_store(out + (size_t)g * xyzz_words<F>(), acc);
+  if (threadIdx.x == 0) xyzz_store(out + (size_t)blockIdx.x * xyzz_words<F>(), acc);
 }
 
 // export: XYZZ (device form) -> canonical reference-form coordinates, 4 x NP64 u64
@@ -421,7 +413,7 @@ static MsmShape make_shape(int n, int c, int nl) {
   s.logS = ilog2((unsigned)s.S);
   s.J = s.logS + 1;
   s.CH = 64;   // entries per thread in the level-0 accumulation
-  s.SCH = 32;  // items per thread in the stitch levels
+  s.SCH = 8;   // items per thread in the stitch levels (mostly pairs: keep it wide)
   s.CH2 = 16;
   s.nchunk = (s.S + s.CH2 - 1) / s.CH2;
   return s;
@@ -453,7 +445,7 @@ static size_t workspace_bytes(const MsmShape &s) {
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
   add((size_t)s.W * s.S * xw * 2);        // T, R
-  add((size_t)s.W * s.J * s.nchunk * xw * 2);  // bitsum + sumseg ping-pong
+  add((size_t)s.W * s.J * xw);               // per-(window, job) sums
   add((size_t)s.W * s.J * 4 * C::NP64 * 8);    // export
   add(cub > cub2 ? cub : cub2);
   return bytes + (1 << 20);
@@ -515,8 +507,7 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   uint32_t *buckets = dev.arena.take<uint32_t>(nb * xw);
   uint32_t *T = dev.arena.take<uint32_t>((size_t)s.W * s.S * xw);
   uint32_t *R = dev.arena.take<uint32_t>((size_t)s.W * s.S * xw);
-  uint32_t *P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * s.nchunk * xw);
-  uint32_t *P1 = dev.arena.take<uint32_t>((size_t)s.W * s.J * s.nchunk * xw);
+  uint32_t *P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * xw);
   uint64_t *exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
   size_t cub = 0, cub2 = 0;
   const int kbits = key_bits(nb);
@@ -565,6 +556,11 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
                          (uint32_t)nb, s.SCH, buckets, outK, outV, (uint32_t)nout);
       ZK_CHECK(hipGetLastError());
       if (final_level) break;
+      // most levels past the first are empty for well-spread scalars: check and stop
+      uint32_t *hc = reinterpret_cast<uint32_t *>(dev.host_staging(4));
+      ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
+      ZK_CHECK(hipStreamSynchronize(st));
+      if (*hc <= (uint32_t)s.SCH) break;  // this level's stitch had one chunk: all complete
       inK = outK; inV = outV; inCount = nullptr; slots = nout;
       uint32_t *tk = outK, *tv = outV;
       outK = altK; outV = altV; altK = tk; altV = tv;
@@ -574,20 +570,13 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
                      s.L, T, R);
   ZK_CHECK(hipGetLastError());
   const int ngrp = s.W * s.J;
-  hipLaunchKernelGGL(k_bitsum<C>, dim3(div_up((size_t)ngrp * s.nchunk, 256)), dim3(256), 0, st, T, R, s.W, s.S,
-                     s.logS, s.CH2, s.nchunk, P0);
-  ZK_CHECK(hipGetLastError());
-  int cur = s.nchunk;
-  uint32_t *src = P0, *dst = P1;
-  while (cur > 1) {
-    const int G = 4;  // narrow levels: depth G each; G=4 minimises total serial depth
-    const int nout = (cur + G - 1) / G;
-    hipLaunchKernelGGL(k_sumseg<C>, dim3(div_up((size_t)ngrp * nout, 256)), dim3(256), 0, st, src, ngrp, cur, G,
-                       dst);
+  {
+    const size_t lds = (size_t)(JT / 2) * xyzz_words<F>() * 4;
+    ZK_CHECK(hipFuncSetAttribute((const void *)k_jobsum<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_jobsum<C>, dim3(ngrp), dim3(JT), lds, st, T, R, s.S, s.logS, P0);
     ZK_CHECK(hipGetLastError());
-    cur = nout;
-    uint32_t *tmp = src; src = dst; dst = tmp;
   }
+  uint32_t *src = P0;
   hipLaunchKernelGGL(k_export<C>, dim3(div_up(ngrp, 64)), dim3(64), 0, st, src, ngrp, exp);
   ZK_CHECK(hipGetLastError());
   const size_t expbytes = (size_t)ngrp * 4 * C::NP64 * 8;

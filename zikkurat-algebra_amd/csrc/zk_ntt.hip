@@ -116,6 +116,35 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int
   const int R = 1 << r;
   const int tid = threadIdx.x;
   int s = 0;
+  if (r >= 2) {  // first radix-4 round: twiddles w_2^0 = w_4^0 = 1, only w_4^1 is non-trivial
+    const int q4 = R >> 2;
+    Fe<F> w3;
+    lds_get(w3, itw + (size_t)(R / 4) * NW);  // w_4 = w_R^(R/4)
+    for (int u = tid; u < G * q4; u += NTT_THREADS) {
+      const int g = u / q4, j = u % q4;
+      const int i0 = g * R + j * 4;
+      Fe<F> a0, a1, a2, a3, b0, b1, b2, b3, t;
+      lds_get(a0, data + (size_t)i0 * NW);
+      lds_get(a1, data + (size_t)(i0 + 1) * NW);
+      lds_get(a2, data + (size_t)(i0 + 2) * NW);
+      lds_get(a3, data + (size_t)(i0 + 3) * NW);
+      fe_add(b0, a0, a1);
+      fe_sub(b1, a0, a1);
+      fe_add(b2, a2, a3);
+      fe_sub(b3, a2, a3);
+      fe_add(a0, b0, b2);
+      fe_sub(a2, b0, b2);
+      fe_mul(t, b3, w3);
+      fe_add(a1, b1, t);
+      fe_sub(a3, b1, t);
+      lds_put(data + (size_t)i0 * NW, a0);
+      lds_put(data + (size_t)(i0 + 1) * NW, a1);
+      lds_put(data + (size_t)(i0 + 2) * NW, a2);
+      lds_put(data + (size_t)(i0 + 3) * NW, a3);
+    }
+    __syncthreads();
+    s = 2;
+  }
   for (; s + 1 < r; s += 2) {  // radix-4 rounds: stages s and s+1
     const int half = 1 << s;
     const int q4 = R >> 2;

@@ -45,6 +45,7 @@ EXTENSION_SYMBOLS = [
     "zkg_memcpy_htod", "zkg_memcpy_dtoh", "zkg_device_synchronize", "zkg_g1_msm_device", "zkg_ntt_device",
     "zkg_g1_proj_add", "zkg_g1_proj_normalize", "zkg_g1_proj_to_affine", "zkg_gen_fr", "zkg_gen_g1_points",
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
+    "zkg_field_mul_rate",
 ]
 
 _lib = None
@@ -70,6 +71,8 @@ def load():
         lib.zkg_gen_fr.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, U64P]
         lib.zkg_gen_g1_points.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, U64P]
         lib.zkg_timer_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]
+        lib.zkg_field_mul_rate.restype = ctypes.c_double
+        lib.zkg_field_mul_rate.argtypes = [ctypes.c_int]
         _lib = lib
     return _lib
 
@@ -281,6 +284,14 @@ def msm_device(curve, n, d_scalars, d_points, mont=True, window=0):
 def ntt_device(curve, m, gen, d_src, d_dst, inverse=False):
     load().zkg_ntt_device(CURVE_ID[curve], 1 if inverse else 0, m, _p(np.ascontiguousarray(gen)), d_src.ptr,
                           d_dst.ptr)
+
+
+FIELD_ID = {("bn128", "fp"): 0, ("bn128", "fr"): 1, ("bls12_381", "fp"): 2, ("bls12_381", "fr"): 3}
+
+
+def field_mul_rate(curve, field):
+    """measured Montgomery products/s of the device field engine (VALU roofline probe)"""
+    return load().zkg_field_mul_rate(FIELD_ID[(curve, field)])
 
 
 def timer(enable=None, reset=False):

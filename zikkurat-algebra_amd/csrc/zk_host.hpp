@@ -277,4 +277,84 @@ template <class F> inline void proj_scale(Proj<F> &r, const Proj<F> &P, const ui
   r = acc;
 }
 
+// ---------------------------------------------------------------------------
+// G1 in extended Jacobian "XYZZ" coordinates (x = X/ZZ, y = Y/ZZZ), a = 0 -- the
+// form the device bucket sums arrive in; used for the host Horner combine.
+// Infinity: ZZ == 0.  Curves here have no 2-torsion (odd group order), so Y != 0
+// for every finite point.
+template <class F>
+struct Xyzz {
+  Fe<F> X, Y, ZZ, ZZZ;
+};
+template <class F> inline void xyzz_set_inf(Xyzz<F> &r) {
+  set_one(r.X);
+  set_one(r.Y);
+  set_zero(r.ZZ);
+  set_zero(r.ZZZ);
+}
+template <class F> inline bool xyzz_is_inf(const Xyzz<F> &a) { return is_zero(a.ZZ); }
+// r = 2p (dbl-2008-s-1): 6M + 3S
+template <class F> inline void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &p) {
+  if (xyzz_is_inf(p)) { r = p; return; }
+  Fe<F> U, V, W, S, M, t, X3;
+  add(U, p.Y, p.Y);
+  sqr(V, U);
+  mul(W, U, V);
+  mul(S, p.X, V);
+  sqr(t, p.X);
+  add(M, t, t);
+  add(M, M, t);
+  sqr(t, M);
+  sub(t, t, S);
+  sub(X3, t, S);
+  sub(t, S, X3);
+  mul(t, M, t);
+  mul(U, W, p.Y);
+  sub(r.Y, t, U);
+  r.X = X3;
+  mul(r.ZZ, V, p.ZZ);
+  mul(r.ZZZ, W, p.ZZZ);
+}
+// r = a + b (add-2008-s), all special cases
+template <class F> inline void xyzz_add(Xyzz<F> &r, const Xyzz<F> &a, const Xyzz<F> &b) {
+  if (xyzz_is_inf(b)) { r = a; return; }
+  if (xyzz_is_inf(a)) { r = b; return; }
+  Fe<F> U1, U2, S1, S2, P, R;
+  mul(U1, a.X, b.ZZ);
+  mul(U2, b.X, a.ZZ);
+  mul(S1, a.Y, b.ZZZ);
+  mul(S2, b.Y, a.ZZZ);
+  sub(P, U2, U1);
+  sub(R, S2, S1);
+  if (is_zero(P)) {
+    if (is_zero(R)) xyzz_dbl(r, a);
+    else xyzz_set_inf(r);
+    return;
+  }
+  Fe<F> PP, PPP, Q, t, X3;
+  sqr(PP, P);
+  mul(PPP, P, PP);
+  mul(Q, U1, PP);
+  sqr(t, R);
+  sub(t, t, PPP);
+  sub(t, t, Q);
+  sub(X3, t, Q);
+  sub(t, Q, X3);
+  mul(t, R, t);
+  mul(S1, S1, PPP);
+  sub(r.Y, t, S1);
+  r.X = X3;
+  mul(t, a.ZZ, b.ZZ);
+  mul(r.ZZ, t, PP);
+  mul(t, a.ZZZ, b.ZZZ);
+  mul(r.ZZZ, t, PPP);
+}
+// -> homogeneous projective (X ZZZ : Y ZZ : ZZ ZZZ)
+template <class F> inline void xyzz_to_proj(Proj<F> &r, const Xyzz<F> &a) {
+  if (xyzz_is_inf(a)) { proj_set_inf(r); return; }
+  mul(r.X, a.X, a.ZZZ);
+  mul(r.Y, a.Y, a.ZZ);
+  mul(r.Z, a.ZZ, a.ZZZ);
+}
+
 }  // namespace zkh

@@ -8,9 +8,13 @@
 //
 //   0. k_points_int affine points -> internal radix (one product per coordinate)
 //   1. k_digits     scalar (Montgomery -> standard by REDC, Fr_mont.c:330-335) ->
-//                   signed c-bit digits for all W windows -> (bucket key, index|sign)
-//   2. sort         LSD radix sort of the W*n pairs by bucket key (hipCUB onesweep)
-//   3. k_offsets    bucket start offsets from the sorted keys
+//                   signed c-bit digits for all W windows -> (key, index|sign), key =
+//                   window << c | (|digit| - 1); keys are emitted window-major
+//   2. sort         LSD radix sort of the W*n pairs on the c in-window bits only
+//                   (hipCUB onesweep, 2 passes at c = 16): the sort is stable, so
+//                   equal digits stay window-major and every (window, digit) bucket is
+//                   one contiguous run, ordered by rank = digit * W + window
+//   3. k_offsets    bucket start offsets (per rank) from the sorted keys
 //   4. k_accum      balanced bucket accumulation: every thread adds exactly CH
 //                   consecutive sorted entries (mixed XYZZ += affine adds), flushing
 //                   complete runs to their bucket and boundary runs as partial items
@@ -27,6 +31,8 @@
 // wavefront's serial chain of 381-bit point adds is slow on CDNA4, so the
 // deep-but-narrow tail runs on one host core (step 9).
 #include <hipcub/hipcub.hpp>
+#include <chrono>
+#include <vector>
 #include "zk_curve.hpp"
 #include "zk_host.hpp"
 #include "zk_runtime.hpp"
@@ -67,8 +73,8 @@ __global__ void __launch_bounds__(256) k_points_int(const uint64_t *__restrict__
 
 // ---------------------------------------------------------------------------
 // 1. digits -> (key, value) pairs for the bucket sort.
-//    key = w * B + (|digit| - 1), or nb (sentinel, sorts last) for a zero digit
-//    value = point index | sign << 31
+//    key = w << c | (|digit| - 1), or w << c | B (sorts after every digit) for a zero
+//    digit; value = point index | sign << 31
 template <class C>
 __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int nl, int mont,
                                                 int c, int W, uint32_t *__restrict__ keys,
@@ -95,7 +101,6 @@ __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ sca
   const uint32_t B = 1u << (c - 1);
   const uint32_t full = 1u << c;
   const uint32_t mask = full - 1;
-  const uint32_t nb = (uint32_t)W * B;
   uint32_t carry = 0;
   for (int w = 0; w < W; w++) {
     uint32_t raw = (k[0] & mask) + carry;
@@ -112,21 +117,29 @@ __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ sca
       sign = 0;
       carry = 0;
     }
-    keys[(size_t)w * n + i] = mag ? (uint32_t)w * B + mag - 1 : nb;
+    keys[(size_t)w * n + i] = ((uint32_t)w << c) | (mag ? mag - 1 : B);
     vals[(size_t)w * n + i] = (uint32_t)i | sign;
   }
 }
 
-// 3. bucket offsets from the sorted keys: offsets[b] = first position with key >= b,
-//    one binary search per bucket (no serial loops, whatever the key distribution)
+// 3. bucket offsets from the sorted keys: offsets[b] = first position whose rank is
+//    >= b, rank = digit * W + window (zero digits rank >= nb), one binary search per
+//    bucket (no serial loops, whatever the key distribution)
+__device__ __forceinline__ uint32_t key_rank(uint32_t key, int c, uint32_t W) {
+  return (key & ((1u << c) - 1)) * W + (key >> c);
+}
+// storage slot of the bucket with rank b (window-major: w * B + digit)
+__device__ __forceinline__ uint32_t bucket_slot(uint32_t b, uint32_t W, uint32_t B) {
+  return (b % W) * B + b / W;
+}
 __global__ void __launch_bounds__(256) k_offsets(const uint32_t *__restrict__ skeys, uint32_t M, uint32_t nb,
-                                                 uint32_t *__restrict__ offsets) {
+                                                 int c, uint32_t W, uint32_t *__restrict__ offsets) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b > nb) return;
-  uint32_t lo = 0, hi = M;  // first index in [lo, hi] with key >= b
+  uint32_t lo = 0, hi = M;  // first index in [lo, hi] with rank >= b
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (skeys[mid] < b) lo = mid + 1; else hi = mid;
+    if (key_rank(skeys[mid], c, W) < b) lo = mid + 1; else hi = mid;
   }
   offsets[b] = lo;
 }
@@ -162,7 +175,7 @@ template <class C>
 __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ points,
                                                const uint32_t *__restrict__ list,
                                                const uint32_t *__restrict__ offsets, uint32_t nb,
-                                               int CH, uint32_t *__restrict__ buckets,
+                                               int CH, uint32_t W, uint32_t B, uint32_t *__restrict__ buckets,
                                                uint32_t *__restrict__ ikeys, uint32_t *__restrict__ ivals,
                                                uint32_t nslots) {
   using F = typename C::Fp;
@@ -184,7 +197,7 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
           xyzz_store(ivals + (size_t)(2 * t) * xyzz_words<F>(), acc);
           k0 = b;
         } else {
-          xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+          xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
         }
         first_run = false;
         xyzz_set_inf(acc);
@@ -201,7 +214,7 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
       xyzz_store(ivals + (size_t)slot * xyzz_words<F>(), acc);
       if (first_run) k0 = b; else k1 = b;
     } else {
-      xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+      xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
     }
   }
   ikeys[2 * t] = k0;
@@ -241,7 +254,7 @@ __global__ void __launch_bounds__(256) k_item_compact(const uint32_t *__restrict
 template <class C>
 __global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
                                                 const uint32_t *__restrict__ count, uint32_t nb, int CH,
-                                                uint32_t *__restrict__ buckets, uint32_t *__restrict__ okeys,
+                                                uint32_t W, uint32_t B, uint32_t *__restrict__ buckets, uint32_t *__restrict__ okeys,
                                                 uint32_t *__restrict__ ovals, uint32_t nslots) {
   using F = typename C::Fp;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -263,7 +276,7 @@ __global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ key
           xyzz_store(ovals + (size_t)(2 * t) * xyzz_words<F>(), acc);
           k0 = b;
         } else {
-          xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+          xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
         }
         first_run = false;
         xyzz_set_inf(acc);
@@ -279,80 +292,140 @@ __global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ key
       xyzz_store(ovals + (size_t)slot * xyzz_words<F>(), acc);
       if (first_run) k0 = b; else k1 = b;
     } else {
-      xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
+      xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
     }
   }
   okeys[2 * t] = k0;
   okeys[2 * t + 1] = k1;
 }
 
-// 6. per (window, segment): T = sum B_m, R = sum (m - lo + 1) B_m over L buckets
-template <class C>
-__global__ void __launch_bounds__(256) k_seg(const uint32_t *__restrict__ buckets,
-                                             const uint32_t *__restrict__ offsets, int W, int B, int L,
-                                             uint32_t *__restrict__ Tout, uint32_t *__restrict__ Rout) {
-  using F = typename C::Fp;
-  const int S = B / L;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= W * S) return;
-  const int w = g / S, s = g % S;
-  Xyzz<F> T, R;
-  xyzz_set_inf(T);
-  xyzz_set_inf(R);
-  for (int m = L - 1; m >= 0; m--) {
-    const size_t b = (size_t)w * B + (size_t)s * L + m;
-    if (offsets[b + 1] > offsets[b]) {  // empty buckets hold garbage (never written)
-      Xyzz<F> bm;
-      xyzz_load(bm, buckets + b * xyzz_words<F>());
-      xyzz_add(T, bm);
-    }
-    xyzz_add(R, T);
+// In-wavefront segmented point sum: the G lanes of an aligned segment (G a power of two
+// <= 64) fold their accumulators with log2(G) cross-lane steps; lane 0 of the segment
+// ends up with the segment's sum.  (Every lane executes every step, so the cost is
+// log2(G) point adds of latency whatever the segment size.)
+template <class F>
+__device__ __forceinline__ Xyzz<F> xyzz_shfl_down(const Xyzz<F> &a, int off, int width) {
+  Xyzz<F> r;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {
+    r.X.v[i] = (uint32_t)__shfl_down((int)a.X.v[i], off, width);
+    r.Y.v[i] = (uint32_t)__shfl_down((int)a.Y.v[i], off, width);
+    r.ZZ.v[i] = (uint32_t)__shfl_down((int)a.ZZ.v[i], off, width);
+    r.ZZZ.v[i] = (uint32_t)__shfl_down((int)a.ZZZ.v[i], off, width);
   }
-  xyzz_store(Tout + (size_t)g * xyzz_words<F>(), T);
-  xyzz_store(Rout + (size_t)g * xyzz_words<F>(), R);
+  return r;
+}
+template <class F>
+__device__ __forceinline__ void seg_fold(Xyzz<F> &acc, int G) {
+  for (int off = G >> 1; off >= 1; off >>= 1) {
+    Xyzz<F> o = xyzz_shfl_down(acc, off, G);
+    xyzz_add(acc, o);
+  }
 }
 
-// 7. one workgroup per (window, job): job j < logS sums U_j = sum_{s: bit j of s} T_s,
-//    job logS sums R_s.  Each thread first adds a strided share of the job's items, then
-//    the workgroup folds the partials with an LDS tree: serial depth ~ items/JT + log2(JT)
-//    point adds (the narrow tail of the reduction is latency bound on CDNA4).
-constexpr int JT = 256;
+// Segment layout shared by the two reduction kernels: per window, segments of
+// decreasing size G (aligned by construction), the window's lane block padded to a
+// multiple of 64 so no wavefront spans two windows.
+struct SegRegion {
+  int count;  // segments in this region
+  int G;      // lanes per segment
+  int len;    // items per segment
+};
+
+// 6. digit split of the bucket weights.  Bucket m of a window (digit m + 1) has
+//    m = m1 * 2^l0 + m0 (l0 + l1 = c - 1), so
+//       sum_m (m+1) B_m = sum_v v Y0_v + 2^l0 sum_v v Y1_v + sum_v Y0_v,
+//       Y0_v = sum_{m0 = v} B_m (2^l1 buckets),  Y1_v = sum_{m1 = v} B_m (2^l0 buckets).
+//    Every Y is a PLAIN sum (no weights, no running-sum chain): G lanes per Y, each adds
+//    len/G buckets, then an in-wavefront fold.  Region 0: the 2^l1 sums Y1 (longer
+//    segments first), region 1: the 2^l0 sums Y0.  Output Y[w][y]: y < 2^l0 -> Y0_y,
+//    else Y1_(y - 2^l0).
 template <class C>
-__global__ void __launch_bounds__(JT) k_jobsum(const uint32_t *__restrict__ T, const uint32_t *__restrict__ R,
-                                              int S, int logS, uint32_t *__restrict__ out) {
+__global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ buckets,
+                                              const uint32_t *__restrict__ offsets, int W, int c, int l0,
+                                              SegRegion r0, SegRegion r1, int wlanes,
+                                              uint32_t *__restrict__ Y) {
   using F = typename C::Fp;
-  extern __shared__ uint32_t lds[];
-  const int J = logS + 1;
-  const int w = blockIdx.x / J, j = blockIdx.x % J;
-  const int n = (j < logS) ? (S >> 1) : S;
+  const int l1 = c - 1 - l0;
+  const int NY = (1 << l0) + (1 << l1);
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int w = g / wlanes, t = g % wlanes;  // W * wlanes is a multiple of 256 by launch
+  const bool active = w < W;
+  const int n0 = r0.count * r0.G;
+  int G, len, seg, lane;
+  bool hiY;  // Y1 (region 0) or Y0 (region 1)
+  if (t < n0) { G = r0.G; len = r0.len; seg = t / G; lane = t % G; hiY = true; }
+  else if (t < n0 + r1.count * r1.G) { G = r1.G; len = r1.len; seg = (t - n0) / G; lane = (t - n0) % G; hiY = false; }
+  else { G = 1; len = 0; seg = 0; lane = 0; hiY = false; }  // padding lanes: no fold
+  const uint32_t B = 1u << (c - 1);
+  const int per = len / G;
   Xyzz<F> acc;
   xyzz_set_inf(acc);
-  for (int e = threadIdx.x; e < n; e += JT) {
-    Xyzz<F> p;
-    if (j < logS) {
-      const int lowmask = (1 << j) - 1;
-      const int s = ((e & ~lowmask) << 1) | (1 << j) | (e & lowmask);
-      xyzz_load(p, T + ((size_t)w * S + s) * xyzz_words<F>());
-    } else {
-      xyzz_load(p, R + ((size_t)w * S + e) * xyzz_words<F>());
+  if (active) {
+    for (int k = 0; k < per; k++) {
+      const int s = lane * per + k;
+      const uint32_t m = hiY ? ((uint32_t)seg << l0) + s : ((uint32_t)s << l0) + seg;
+      const uint32_t rank = m * (uint32_t)W + (uint32_t)w;
+      if (offsets[rank + 1] > offsets[rank]) {  // empty buckets hold garbage (never written)
+        Xyzz<F> bm;
+        xyzz_load(bm, buckets + ((size_t)w * B + m) * xyzz_words<F>());
+        xyzz_add(acc, bm);
+      }
     }
-    xyzz_add(acc, p);
   }
-  int active = min(JT, n);
-  for (int stride = JT / 2; stride >= 1; stride >>= 1) {
-    if (stride >= active) continue;  // uniform across the block
-    if (threadIdx.x >= stride && threadIdx.x < 2 * stride && threadIdx.x < active)
-      xyzz_store(lds + (size_t)(threadIdx.x - stride) * xyzz_words<F>(), acc);
-    __syncthreads();
-    if (threadIdx.x < stride && threadIdx.x + stride < active) {
+  seg_fold(acc, G);
+  if (active && lane == 0 && len > 0) {
+    const int y = hiY ? (1 << l0) + seg : seg;
+    xyzz_store(Y + ((size_t)w * NY + y) * xyzz_words<F>(), acc);
+  }
+}
+
+// 7. weighted sums of the Y's by bits: per window, job (d, b) for b < l_d is
+//    U_{d,b} = sum_{v: bit b of v} Yd_v (2^(l_d - 1) items) and one job is sum_v Y0_v
+//    (2^l0 items); J = l0 + l1 + 1 = c jobs.  Same segment scheme: jobs ordered by
+//    length (total, then the l0 jobs over Y0, then the l1 jobs over Y1), G lanes each.
+//    Output P[w][j]: j = 0 total, 1..l0 -> (0, j-1), l0+1.. -> (1, j-1-l0).
+template <class C>
+__global__ void __launch_bounds__(256) k_jobsum(const uint32_t *__restrict__ Y, int W, int c, int l0, int QA,
+                                                int wlanes, uint32_t *__restrict__ out) {
+  using F = typename C::Fp;
+  const int l1 = c - 1 - l0;
+  const int NY = (1 << l0) + (1 << l1);
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int w = g / wlanes, t = g % wlanes;
+  const bool active = w < W;
+  // job j: length n_j, segment size G_j = clamp(n_j / QA, 1, 64); lane offset = prefix sum
+  int j = -1, G = 1, lane = 0, off = 0;  // padding lanes: no job, no fold
+  for (int jj = 0; jj < c; jj++) {
+    const int n = jj == 0 ? (1 << l0) : (jj <= l0 ? (1 << (l0 - 1)) : (1 << (l1 - 1)));
+    int Gj = n / QA;
+    Gj = Gj < 1 ? 1 : (Gj > 64 ? 64 : Gj);
+    if (t >= off && t < off + Gj) { j = jj; G = Gj; lane = t - off; }
+    off += Gj;
+  }
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  if (active && j >= 0) {
+    const int d = (j == 0 || j <= l0) ? 0 : 1;
+    const int b = j == 0 ? -1 : (d == 0 ? j - 1 : j - 1 - l0);
+    const int ld = d ? l1 : l0;
+    const int n = (b < 0) ? (1 << ld) : (1 << (ld - 1));
+    const int per = n / G;
+    const uint32_t *Yd = Y + ((size_t)w * NY + (d ? (1 << l0) : 0)) * xyzz_words<F>();
+    for (int k = 0; k < per; k++) {
+      const int e = lane * per + k;
+      int v = e;
+      if (b >= 0) {
+        const int lowmask = (1 << b) - 1;
+        v = ((e & ~lowmask) << 1) | (1 << b) | (e & lowmask);
+      }
       Xyzz<F> p;
-      xyzz_load(p, lds + (size_t)threadIdx.x * xyzz_words<F>());
+      xyzz_load(p, Yd + (size_t)v * xyzz_words<F>());
       xyzz_add(acc, p);
     }
-    __syncthreads();
-    active = stride;
   }
-  if (threadIdx.x == 0) xyzz_store(out + (size_t)blockIdx.x * xyzz_words<F>(), acc);
+  seg_fold(acc, G);
+  if (active && j >= 0 && lane == 0) xyzz_store(out + ((size_t)w * c + j) * xyzz_words<F>(), acc);
 }
 
 // export: XYZZ (device form) -> canonical reference-form coordinates, 4 x NP64 u64
@@ -378,17 +451,18 @@ __global__ void k_export(const uint32_t *__restrict__ in, int n, uint64_t *__res
 // ---------------------------------------------------------------------------
 // host orchestration
 
-static int key_bits(size_t nb) {  // keys are in [0, nb]
-  int b = 1;
-  while (((size_t)1 << b) <= nb) b++;
-  return b;
-}
-
 struct MsmShape {
-  int n, c, W, B, L, S, logS, J, CH, CH2, nchunk, SCH;
+  int n, c, W, B, l0, l1, NY, QY, J, CH, SCH, QA;
+  SegRegion r0, r1;
+  int ylanes, jlanes;  // lanes per window of k_ysum / k_jobsum (multiples of 64)
 };
 
 static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; return r; }
+
+static int env_int(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
 
 int msm_default_window(int n) {
   // GPU window: more buckets are cheap on a wide device, fewer windows save
@@ -402,20 +476,36 @@ int msm_default_window(int n) {
   return c;
 }
 
-static MsmShape make_shape(int n, int c, int nl) {
+// bits: bit length bound of the scalars (255/254 for canonical Montgomery-path scalars
+// after REDC, 64*nl for std scalars, which are used verbatim).  Signed digits need
+// floor(bits/c) + 1 windows: the top window then holds at most c-1 bits plus the carry,
+// i.e. a digit <= 2^(c-1) = B, so no carry leaves it.
+static MsmShape make_shape(int n, int c, int bits) {
+  static const int envQY = env_int("ZK_MSM_QY", 0), envQA = env_int("ZK_MSM_QA", 0);
   MsmShape s;
   s.n = n;
   s.c = c;
-  s.W = (64 * nl) / c + 1;  // signed digits: one extra window absorbs the final carry
+  s.W = bits / c + 1;
   s.B = 1 << (c - 1);
-  s.L = s.B >= 8 ? 4 : (s.B >= 2 ? s.B / 2 : 1);
-  s.S = s.B / s.L;
-  s.logS = ilog2((unsigned)s.S);
-  s.J = s.logS + 1;
+  s.l0 = c / 2;  // l0 + l1 = c - 1, l0 >= l1
+  s.l1 = c - 1 - s.l0;
+  s.NY = (1 << s.l0) + (1 << s.l1);
+  auto pow2 = [](int v) { int r = 1; while (2 * r <= v) r *= 2; return r; };  // segments need powers of 2
+  s.QY = envQY > 0 ? pow2(envQY) : 16;  // buckets per lane in the Y sums (swept on MI355X)
+  auto clampG = [](int g) { return g < 1 ? 1 : (g > 64 ? 64 : g); };
+  s.r0 = SegRegion{1 << s.l1, clampG((1 << s.l0) / s.QY), 1 << s.l0};  // Y1 sums
+  s.r1 = SegRegion{1 << s.l0, clampG((1 << s.l1) / s.QY), 1 << s.l1};  // Y0 sums
+  s.ylanes = (s.r0.count * s.r0.G + s.r1.count * s.r1.G + 63) & ~63;
+  s.J = c;
   s.CH = 64;   // entries per thread in the level-0 accumulation
   s.SCH = 8;   // items per thread in the stitch levels (mostly pairs: keep it wide)
-  s.CH2 = 16;
-  s.nchunk = (s.S + s.CH2 - 1) / s.CH2;
+  s.QA = envQA > 0 ? pow2(envQA) : 8;  // items per lane in the weighted job sums
+  s.jlanes = 0;
+  for (int j = 0; j < c; j++) {  // same job order / sizes as k_jobsum
+    const int n = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
+    s.jlanes += clampG(n / s.QA);
+  }
+  s.jlanes = (s.jlanes + 63) & ~63;
   return s;
 }
 
@@ -431,8 +521,7 @@ static size_t workspace_bytes(const MsmShape &s) {
   const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s);
   size_t cub = 0, cub2 = 0;
   ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                              (uint32_t *)nullptr, (uint32_t *)nullptr, (int)maxent, 0,
-                                              key_bits(nb)));
+                                              (uint32_t *)nullptr, (uint32_t *)nullptr, (int)maxent, 0, s.c));
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)ns0));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
@@ -444,12 +533,45 @@ static size_t workspace_bytes(const MsmShape &s) {
   add(ns0 * (xw + 4) * 2 + ns0 * 8 + 64); // level-0 items, compacted items, flags, pos, count
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
-  add((size_t)s.W * s.S * xw * 2);        // T, R
+  add((size_t)s.W * s.NY * xw);              // Y
   add((size_t)s.W * s.J * xw);               // per-(window, job) sums
   add((size_t)s.W * s.J * 4 * C::NP64 * 8);    // export
   add(cub > cub2 ? cub : cub2);
   return bytes + (1 << 20);
 }
+
+// opt-in phase profile (env ZK_MSM_PROFILE=1): HIP events between the phases of one
+// call, printed to stderr with the host-side finish time.  Off by default.
+struct PhaseProf {
+  bool on = false;
+  hipStream_t st = nullptr;
+  std::vector<std::pair<const char *, hipEvent_t>> ev;
+  explicit PhaseProf(hipStream_t s) : st(s) {
+    static const int enabled = env_int("ZK_MSM_PROFILE", 0);
+    on = enabled != 0;
+    mark("start");
+  }
+  void mark(const char *name) {
+    if (!on) return;
+    hipEvent_t e;
+    ZK_CHECK(hipEventCreate(&e));
+    ZK_CHECK(hipEventRecord(e, st));
+    ev.emplace_back(name, e);
+  }
+  void report(double host_ms) {
+    if (!on) return;
+    ZK_CHECK(hipStreamSynchronize(st));
+    fprintf(stderr, "[zk msm]");
+    for (size_t i = 1; i < ev.size(); i++) {
+      float ms = 0;
+      ZK_CHECK(hipEventElapsedTime(&ms, ev[i - 1].second, ev[i].second));
+      fprintf(stderr, " %s=%.3f", ev[i].first, ms);
+    }
+    fprintf(stderr, " host_finish=%.3f ms\n", host_ms);
+    for (auto &e : ev) ZK_CHECK(hipEventDestroy(e.second));
+    ev.clear();
+  }
+};
 
 template <class C>
 static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<typename HostOf<C>::Fp> &out);
@@ -469,7 +591,7 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
   ZK_REQUIRE(nl >= 1 && nl <= 4, "msm: expo_nlimbs must be in 1..4 (scalars up to 256 bits)");
   ZK_REQUIRE(!mont || nl == 4, "msm: Montgomery coefficients must have expo_nlimbs == 4");
-  MsmShape s = make_shape(n, c, nl);
+  MsmShape s = make_shape(n, c, mont ? HostOf<C>::Fr::BITS : 64 * nl);
   const size_t nb = (size_t)s.W * s.B;
   const size_t xw = xyzz_words<F>();
   hipStream_t st = dev.stream;
@@ -505,36 +627,40 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   uint32_t *okB = dev.arena.take<uint32_t>(ns1);
   uint32_t *ovB = dev.arena.take<uint32_t>(ns1 * xw);
   uint32_t *buckets = dev.arena.take<uint32_t>(nb * xw);
-  uint32_t *T = dev.arena.take<uint32_t>((size_t)s.W * s.S * xw);
-  uint32_t *R = dev.arena.take<uint32_t>((size_t)s.W * s.S * xw);
+  uint32_t *Y = dev.arena.take<uint32_t>((size_t)s.W * s.NY * xw);
   uint32_t *P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * xw);
   uint64_t *exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
   size_t cub = 0, cub2 = 0;
-  const int kbits = key_bits(nb);
+  const int kbits = c;  // in-window digit bits only (see step 2)
   ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
   if (cub2 > cub) cub = cub2;
   void *cubtmp = dev.arena.take<char>(cub);
 
+  PhaseProf prof(st);
   hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_pt, n, pts_int);
   ZK_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_sc, n, nl, mont ? 1 : 0, c, s.W,
                      keys, vals);
   ZK_CHECK(hipGetLastError());
+  prof.mark("digits");
   ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
+  prof.mark("sort");
   hipLaunchKernelGGL(k_offsets, dim3(div_up(nb + 1, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
-                     (uint32_t)nb, offsets);
+                     (uint32_t)nb, c, (uint32_t)s.W, offsets);
   ZK_CHECK(hipGetLastError());
 
+  prof.mark("offsets");
   KernelTimer &kt = dominant_timer();
   {
     if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev0, st));
     // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
     hipLaunchKernelGGL(k_accum<C>, dim3(div_up(ns0 / 2, 256)), dim3(256), 0, st, pts_int, list, offsets,
-                       (uint32_t)nb, s.CH, buckets, ikeys0, ivals0, (uint32_t)ns0);
+                       (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0, ivals0, (uint32_t)ns0);
     ZK_CHECK(hipGetLastError());
     if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev1, st));
   }
+  prof.mark("accum");
   // stitch levels: compact the partial items, sum them per bucket, repeat
   {
     const uint32_t *inK = ikeys0, *inV = ivals0;
@@ -553,7 +679,7 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
       const bool final_level = slots <= (size_t)s.SCH;  // all items fit one chunk: everything completes
       const size_t nout = final_level ? 2 : 2 * ((slots + s.SCH - 1) / s.SCH);
       hipLaunchKernelGGL(k_stitch<C>, dim3(div_up(nout / 2, 256)), dim3(256), 0, st, ckeys, cvals, ccount,
-                         (uint32_t)nb, s.SCH, buckets, outK, outV, (uint32_t)nout);
+                         (uint32_t)nb, s.SCH, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
       ZK_CHECK(hipGetLastError());
       if (final_level) break;
       // most levels past the first are empty for well-spread scalars: check and stop
@@ -566,15 +692,20 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
       outK = altK; outV = altV; altK = tk; altV = tv;
     }
   }
-  hipLaunchKernelGGL(k_seg<C>, dim3(div_up((size_t)s.W * s.S, 256)), dim3(256), 0, st, buckets, offsets, s.W, s.B,
-                     s.L, T, R);
-  ZK_CHECK(hipGetLastError());
+  prof.mark("stitch");
+  {
+    const size_t lanes = (size_t)s.W * s.ylanes;
+    hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
+                       s.r1, s.ylanes, Y);
+    ZK_CHECK(hipGetLastError());
+    prof.mark("ysum");
+  }
   const int ngrp = s.W * s.J;
   {
-    const size_t lds = (size_t)(JT / 2) * xyzz_words<F>() * 4;
-    ZK_CHECK(hipFuncSetAttribute((const void *)k_jobsum<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_jobsum<C>, dim3(ngrp), dim3(JT), lds, st, T, R, s.S, s.logS, P0);
+    const size_t lanes = (size_t)s.W * s.jlanes;
+    hipLaunchKernelGGL(k_jobsum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, s.jlanes, P0);
     ZK_CHECK(hipGetLastError());
+    prof.mark("jobsum");
   }
   uint32_t *src = P0;
   hipLaunchKernelGGL(k_export<C>, dim3(div_up(ngrp, 64)), dim3(64), 0, st, src, ngrp, exp);
@@ -589,47 +720,47 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
     kt.total_ms += ms;
     kt.launches++;
   }
+  prof.mark("export");
+  const auto t0 = std::chrono::steady_clock::now();
   finish_host<C>(s, h, out);
+  prof.report(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
-// host: combine the per-(window, job) sums:
-//   V_w = sum_s R_s + L * sum_k 2^k U_k ;  result = sum_w 2^(c w) V_w
-// Every term is 2^e * Z with e = c*w (R job) or c*w + log2(L) + k (U_k job); those
-// exponents never collide across windows, so one Horner pass over e does it all.
+// host: combine the per-(window, job) sums (XYZZ, canonical reference form; job order
+// of k_jobsum: total, U_{0,0..l0-1}, U_{1,0..l1-1}):
+//   window w: sum_m (m+1) B_m = sum_b 2^b U_{0,b} + 2^l0 sum_b 2^b U_{1,b} + Total
+//   result  = sum_w 2^(c w) (window sum)
+// Every term is 2^e * Z with e = c w + b, c w + l0 + b or c w (< c (w+1)), so one
+// Horner pass over e (c W - 1 doublings) does it all; on one host core a point op
+// costs ~0.4 us against ~20 us for a lone GPU lane, which is why this serial tail
+// stays here.
 template <class C>
 static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<typename HostOf<C>::Fp> &out) {
   using HF = typename HostOf<C>::Fp;
   const int NP = C::NP64;
-  zkh::Fe<HF> b3;
-  HostOf<C>::b3(b3);
-  const int logL = ilog2((unsigned)s.L);
-  const int emax = s.c * (s.W - 1) + logL + s.logS + 1;
-  std::vector<zkh::Proj<HF>> Z(emax + 1);
-  for (auto &z : Z) zkh::proj_set_inf(z);
+  const int emax = s.c * s.W - 1;
+  std::vector<zkh::Xyzz<HF>> Z(emax + 1);
+  for (auto &z : Z) zkh::xyzz_set_inf(z);
   for (int w = 0; w < s.W; w++) {
     for (int j = 0; j < s.J; j++) {
       const uint64_t *q = exported + ((size_t)w * s.J + j) * 4 * NP;
-      zkh::Fe<HF> X, Y, ZZ, ZZZ;
-      memcpy(X.v, q + 0 * NP, NP * 8);
-      memcpy(Y.v, q + 1 * NP, NP * 8);
-      memcpy(ZZ.v, q + 2 * NP, NP * 8);
-      memcpy(ZZZ.v, q + 3 * NP, NP * 8);
-      if (zkh::is_zero(ZZ)) continue;
-      zkh::Proj<HF> p;  // (X*ZZZ : Y*ZZ : ZZ*ZZZ)
-      zkh::mul(p.X, X, ZZZ);
-      zkh::mul(p.Y, Y, ZZ);
-      zkh::mul(p.Z, ZZ, ZZZ);
-      const int e = (j < s.logS) ? s.c * w + logL + j : s.c * w;
-      zkh::proj_add(Z[e], Z[e], p, b3);
+      zkh::Xyzz<HF> p;
+      memcpy(p.X.v, q + 0 * NP, NP * 8);
+      memcpy(p.Y.v, q + 1 * NP, NP * 8);
+      memcpy(p.ZZ.v, q + 2 * NP, NP * 8);
+      memcpy(p.ZZZ.v, q + 3 * NP, NP * 8);
+      if (zkh::xyzz_is_inf(p)) continue;
+      const int e = s.c * w + (j == 0 ? 0 : j - 1);  // job order of k_jobsum
+      zkh::xyzz_add(Z[e], Z[e], p);
     }
   }
-  zkh::Proj<HF> acc;
-  zkh::proj_set_inf(acc);
+  zkh::Xyzz<HF> acc;
+  zkh::xyzz_set_inf(acc);
   for (int e = emax; e >= 0; e--) {
-    if (!zkh::proj_is_inf(acc)) zkh::proj_dbl(acc, acc, b3);
-    if (!zkh::proj_is_inf(Z[e])) zkh::proj_add(acc, acc, Z[e], b3);
+    zkh::xyzz_dbl(acc, acc);
+    zkh::xyzz_add(acc, acc, Z[e]);
   }
-  out = acc;
+  zkh::xyzz_to_proj(out, acc);
 }
 
 // ---------------------------------------------------------------------------

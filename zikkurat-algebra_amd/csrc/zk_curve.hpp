@@ -132,6 +132,66 @@ __device__ __forceinline__ void xyzz_add_aff(Xyzz<F> &acc, const Aff<F> &a) {
   fe_mul(acc.ZZZ, acc.ZZZ, PPP);
 }
 
+// Bucket-accumulation mixed add for the 381-bit field, with lazy subtractions.
+// Same formula as xyzz_add_aff (madd-2008-s), but every difference is taken lazily
+// (a + K p - b, zk_field.hpp "lazy ops"), the P == 0 / R == 0 tests move onto the
+// squares PP and RR (products are < 2p and normalised, and PP == 0 <=> P == 0 as p is
+// prime), and Y3 = R (Q - X3) - Y1 PPP is one fe_mul2 (shared reduction).
+// Representation invariant of acc between calls: X, Y normalised limbs with values
+// X < 14p, Y < 6p (not < 2p); ZZ, ZZZ < 2p.  xyzz_settle() restores < 2p before the
+// accumulator leaves the kernel.  Bounds (BLS12-381 Fp: 14 x 28-bit limbs, R'/p > 2^11):
+//   P = U2 + 16p - X1 < 18p, limbs < 2^29.6;  R = S2 + 8p - Y1 < 10p
+//   PP, RR, PPP, Q < 2p (products of values < 2^11 p)
+//   X3 = RR + 4p - PPP + 8p - 2Q < 14p;  t = Q + 16p - X3 < 18p
+//   Y3 = (R t + (6p - Y1) PPP) / R' < 2p... then + 0: Y3 < 2p < 6p
+// Column sums in fe_mul2 (R t: limbs < 2^29.6 each; (6p - Y1): < 2^29.6) stay < 2^64.
+template <class F>
+__device__ __forceinline__ void xyzz_add_aff_lazy(Xyzz<F> &acc, const Aff<F> &a) {
+  static_assert(F::N == 14 && F::RB == 28, "lazy madd bounds are derived for the 14 x 28-bit field");
+  if (xyzz_is_inf(acc)) { xyzz_from_aff(acc, a); return; }
+  Fe<F> P, R, PP, RR, t;
+  fe_mul(t, a.x, acc.ZZ);                 // U2
+  fe_sub_lazy<F, 16, 1>(P, t, acc.X);     // P = U2 - X1
+  fe_mul(t, a.y, acc.ZZZ);                // S2
+  fe_sub_lazy<F, 8, 1>(R, t, acc.Y);      // R = S2 - Y1
+  fe_sqr(PP, P);
+  fe_sqr(RR, R);
+  if (fe_is_zero(PP)) {
+    if (fe_is_zero(RR)) { xyzz_dbl_aff(acc, a); }
+    else { xyzz_set_inf(acc); }
+    return;
+  }
+  Fe<F> PPP, Q, X3, q2;
+  fe_mul(PPP, P, PP);
+  fe_mul(Q, acc.X, PP);
+  fe_sub_lazy<F, 4, 1>(t, RR, PPP);       // RR - PPP
+  fe_add_lazy(q2, Q, Q);
+  fe_sub_lazy<F, 8, 2>(X3, t, q2);        // - 2Q
+  fe_norm(X3);
+  fe_sub_lazy<F, 16, 1>(t, Q, X3);        // Q - X3
+  Fe<F> ny;
+  fe_sub_lazy<F, 6, 1>(ny, Fe<F>{}, acc.Y);  // 6p - Y1 (acc.Y < 6p, normalised)
+  fe_mul2(acc.Y, R, t, ny, PPP);          // Y3 = R (Q - X3) - Y1 PPP
+  acc.X = X3;
+  fe_mul(acc.ZZ, acc.ZZ, PP);
+  fe_mul(acc.ZZZ, acc.ZZZ, PPP);
+}
+// bring a lazily accumulated X, Y back below 2p (the form every other kernel expects)
+template <class F>
+__device__ __forceinline__ void xyzz_settle(Xyzz<F> &acc) {
+  if (F::N == 14) {
+    fe_reduce(acc.X);
+    fe_reduce(acc.Y);
+  }
+}
+// dispatch: lazy variant for the 381-bit field, exact variant otherwise (the 254-bit
+// fields have only 3 spare bits per limb and R'/p ~ 2^7.4: not enough for these bounds)
+template <class F>
+__device__ __forceinline__ void xyzz_acc_aff(Xyzz<F> &acc, const Aff<F> &a) {
+  if constexpr (F::N == 14) xyzz_add_aff_lazy(acc, a);
+  else xyzz_add_aff(acc, a);
+}
+
 // acc += b  (add-2008-s), all special cases handled
 template <class F>
 __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {

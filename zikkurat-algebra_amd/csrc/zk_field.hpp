@@ -185,6 +185,47 @@ __device__ __forceinline__ void fe_mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b)
   for (int i = 0; i < N; i++) r.v[i] = o[i];
 }
 
+// r = (a*b + c*d) / R'  -- two products sharing ONE Montgomery reduction (lazy
+// reduction): 2N^2 + N^2 mads instead of 4N^2.  Column sums hold 2N products of each
+// kind, so the operand limbs must be small enough (see callers); inputs whose
+// a*b + c*d < p*R' give an output < 2p.
+template <class F>
+__device__ __forceinline__ void fe_mul2(Fe<F> &r, const Fe<F> &a, const Fe<F> &b, const Fe<F> &c,
+                                        const Fe<F> &d) {
+  constexpr int N = F::N;
+  uint32_t m[N];
+  uint32_t o[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+      acc += (uint64_t)a.v[i] * b.v[k - i];
+      acc += (uint64_t)c.v[i] * d.v[k - i];
+      acc += (uint64_t)m[i] * F::p(k - i);
+    }
+    acc += (uint64_t)a.v[k] * b.v[0];
+    acc += (uint64_t)c.v[k] * d.v[0];
+    m[k] = ((uint32_t)acc * F::MINV) & F::MASK;
+    acc += (uint64_t)m[k] * F::p(0);
+    acc >>= F::RB;
+  }
+#pragma unroll
+  for (int k = N; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = k - N + 1; i < N; i++) {
+      acc += (uint64_t)a.v[i] * b.v[k - i];
+      acc += (uint64_t)c.v[i] * d.v[k - i];
+      acc += (uint64_t)m[i] * F::p(k - i);
+    }
+    o[k - N] = (uint32_t)acc & F::MASK;
+    acc >>= F::RB;
+  }
+  o[N - 1] = (uint32_t)acc;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = o[i];
+}
+
 // squaring: off-diagonal products once, doubled (saves ~N^2/2 mads)
 template <class F>
 __device__ __forceinline__ void fe_sqr(Fe<F> &r, const Fe<F> &a) {
@@ -223,6 +264,56 @@ __device__ __forceinline__ void fe_sqr(Fe<F> &r, const Fe<F> &a) {
   for (int i = 0; i < N; i++) r.v[i] = o[i];
 }
 
+// ---------------------------------------------------------------------------- lazy ops
+// Redundant arithmetic for chains of additions (NTT butterflies).  The unsaturated
+// limbs leave 32 - RB bits of headroom per limb and R'/p >= 2^(RB*N)/p spare value
+// range, so sums need no carry handling and no reduction:
+//   fe_add_lazy  r_i = a_i + b_i
+//   fe_sub_lazy  r_i = a_i + kp_i - b_i, kp = K*p written with "borrowed" limbs
+//                (every limb below the top >= BW*(2^RB - 1)), so no limb goes negative
+//                as long as b's limbs are <= BW*(2^RB - 1) and b's top limb fits.
+//   fe_norm      carry-propagate back to RB-bit limbs (value unchanged)
+// fe_mul accepts one operand with limbs < 2^31 (the column sums stay < 2^64) and maps
+// any value < (R'/p) * p to < 2p when the other operand is < p, which is how the NTT
+// brings lazily-grown values back into range.
+template <class F, int K>
+__host__ __device__ constexpr uint32_t kp_limb(int i) {  // limb i of K*p, RB-bit limbs
+  uint64_t carry = 0;
+  uint32_t out = 0;
+  for (int j = 0; j <= i; j++) {
+    const uint64_t v = (uint64_t)F::p(j) * K + carry;
+    out = (j == F::N - 1) ? (uint32_t)v : (uint32_t)(v & F::MASK);
+    carry = v >> F::RB;
+  }
+  return out;
+}
+template <class F, int K, int BW>
+__host__ __device__ constexpr uint32_t kp_borrowed(int i) {
+  return i == 0 ? kp_limb<F, K>(0) + ((uint32_t)BW << F::RB)
+                : (i < F::N - 1 ? kp_limb<F, K>(i) + ((uint32_t)BW << F::RB) - BW : kp_limb<F, K>(i) - BW);
+}
+template <class F>
+__device__ __forceinline__ void fe_add_lazy(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = a.v[i] + b.v[i];
+}
+template <class F, int K = 4, int BW = 1>
+__device__ __forceinline__ void fe_sub_lazy(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = a.v[i] + kp_borrowed<F, K, BW>(i) - b.v[i];
+}
+template <class F>
+__device__ __forceinline__ void fe_norm(Fe<F> &a) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::N - 1; i++) {
+    const uint32_t v = a.v[i] + c;
+    a.v[i] = v & F::MASK;
+    c = v >> F::RB;
+  }
+  a.v[F::N - 1] += c;
+}
+
 // canonical representative (< p) of a value < 2p
 template <class F>
 __device__ __forceinline__ void fe_canon(Fe<F> &a) {
@@ -237,6 +328,15 @@ __device__ __forceinline__ void fe_canon(Fe<F> &a) {
   const bool lt = c < 0;
 #pragma unroll
   for (int i = 0; i < F::N; i++) a.v[i] = lt ? a.v[i] : d[i];
+}
+
+// any value < (R'/2) (normalised or lazily grown limbs < 2^31) -> same residue, < 2p
+template <class F>
+__device__ __forceinline__ void fe_reduce(Fe<F> &a) {
+  Fe<F> one, t;
+  fe_one(one);
+  fe_mul(t, a, one);
+  a = t;
 }
 
 // ---------------------------------------------------------------------------- radix conversion

@@ -193,6 +193,7 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
     xyzz_set_inf(acc);
     for (uint32_t e = cs; e < ce; e++) {
       if (e >= bend) {  // run of bucket b ends inside the chunk
+        xyzz_settle(acc);
         if (first_run && bbeg < cs) {
           xyzz_store(ivals + (size_t)(2 * t) * xyzz_words<F>(), acc);
           k0 = b;
@@ -206,9 +207,10 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
       Aff<F> P;
       bool inf;
       load_signed_point(P, inf, points, list[e]);
-      if (!inf) xyzz_add_aff(acc, P);
+      if (!inf) xyzz_acc_aff(acc, P);
     }
     // last run: partial if it started before the chunk or continues after it
+    xyzz_settle(acc);
     if (bbeg < cs || bend > ce) {
       const uint32_t slot = first_run ? 2 * t : 2 * t + 1;
       xyzz_store(ivals + (size_t)slot * xyzz_words<F>(), acc);

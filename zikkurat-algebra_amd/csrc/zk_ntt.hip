@@ -109,7 +109,13 @@ __device__ __forceinline__ void lds_put(uint32_t *p, const Fe<F> &x) {
   for (int q = 0; q < F::N; q++) p[q] = x.v[q];
 }
 
-// in-LDS DIT over G instances of R points (bit-reversed input order -> natural order)
+// in-LDS DIT over G instances of R points (bit-reversed input order -> natural order).
+// Lazy butterflies (zk_field.hpp "lazy ops"): x = a + t, y = a + 4p - t with no carries
+// or reductions; limbs are renormalised once per radix-4 round when written back to LDS.
+// Value bound: inputs < p, every stage adds < 4p, so after R = 2^8 points (8 stages)
+// values are < 33p, well inside fe_mul's input range (R'/p > 140): the products of the
+// next stage and the pass's closing product (twiddle / scale / one) bring them back
+// below 2p.  Limb bound: normalised (< 2^29) at round entry, < 2^31.4 at round exit.
 template <class F>
 __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int r, int G) {
   constexpr int NW = F::N;
@@ -123,20 +129,25 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int
     for (int u = tid; u < G * q4; u += NTT_THREADS) {
       const int g = u / q4, j = u % q4;
       const int i0 = g * R + j * 4;
-      Fe<F> a0, a1, a2, a3, b0, b1, b2, b3, t;
+      Fe<F> a0, a1, a2, a3, b0, b1, b3, t;
       lds_get(a0, data + (size_t)i0 * NW);
       lds_get(a1, data + (size_t)(i0 + 1) * NW);
       lds_get(a2, data + (size_t)(i0 + 2) * NW);
       lds_get(a3, data + (size_t)(i0 + 3) * NW);
-      fe_add(b0, a0, a1);
-      fe_sub(b1, a0, a1);
-      fe_add(b2, a2, a3);
-      fe_sub(b3, a2, a3);
-      fe_add(a0, b0, b2);
-      fe_sub(a2, b0, b2);
+      fe_add_lazy(b0, a0, a1);
+      fe_sub_lazy(b1, a0, a1);
+      fe_sub_lazy(b3, a2, a3);
       fe_mul(t, b3, w3);
-      fe_add(a1, b1, t);
-      fe_sub(a3, b1, t);
+      Fe<F> s23;
+      fe_add_lazy(s23, a2, a3);
+      fe_add_lazy(a0, b0, s23);
+      fe_sub_lazy<F, 4, 2>(a2, b0, s23);  // s23 limbs <= 2 (2^RB - 1): borrow 2
+      fe_add_lazy(a1, b1, t);
+      fe_sub_lazy(a3, b1, t);
+      fe_norm(a0);
+      fe_norm(a1);
+      fe_norm(a2);
+      fe_norm(a3);
       lds_put(data + (size_t)i0 * NW, a0);
       lds_put(data + (size_t)(i0 + 1) * NW, a1);
       lds_put(data + (size_t)(i0 + 2) * NW, a2);
@@ -163,18 +174,22 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int
       // stage s
       Fe<F> b0, b1, b2, b3;
       fe_mul(t, a1, w1);
-      fe_add(b0, a0, t);
-      fe_sub(b1, a0, t);
+      fe_add_lazy(b0, a0, t);
+      fe_sub_lazy(b1, a0, t);
       fe_mul(t, a3, w1);
-      fe_add(b2, a2, t);
-      fe_sub(b3, a2, t);
+      fe_add_lazy(b2, a2, t);
+      fe_sub_lazy(b3, a2, t);
       // stage s+1
       fe_mul(t, b2, w2);
-      fe_add(a0, b0, t);
-      fe_sub(a2, b0, t);
+      fe_add_lazy(a0, b0, t);
+      fe_sub_lazy(a2, b0, t);
       fe_mul(t, b3, w3);
-      fe_add(a1, b1, t);
-      fe_sub(a3, b1, t);
+      fe_add_lazy(a1, b1, t);
+      fe_sub_lazy(a3, b1, t);
+      fe_norm(a0);
+      fe_norm(a1);
+      fe_norm(a2);
+      fe_norm(a3);
       lds_put(data + (size_t)i0 * NW, a0);
       lds_put(data + (size_t)(i0 + half) * NW, a1);
       lds_put(data + (size_t)(i0 + 2 * half) * NW, a2);
@@ -194,8 +209,10 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int
       lds_get(b, data + (size_t)(i0 + half) * NW);
       lds_get(w, itw + (size_t)(off * (R / (2 * half))) * NW);
       fe_mul(t, b, w);
-      fe_add(x, a, t);
-      fe_sub(y, a, t);
+      fe_add_lazy(x, a, t);
+      fe_sub_lazy(y, a, t);
+      fe_norm(x);
+      fe_norm(y);
       lds_put(data + (size_t)i0 * NW, x);
       lds_put(data + (size_t)(i0 + half) * NW, y);
     }
@@ -290,6 +307,8 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
     Fe<F> t;
     fe_load_ref(t, scale);
     fe_to_int(sc, t);
+  } else {
+    fe_one(sc);
   }
   for (int e = tid; e < nel; e += NTT_THREADS) {
     const int g = e % G, k = e / G;  // consecutive threads -> consecutive g (coalesced)
@@ -304,11 +323,11 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
       x = y;
     } else {
       addr = (a.P == 1) ? (size_t)k : nat_base + (size_t)(k0base + g) + (size_t)k * a.T;
-      if (scale) {
-        Fe<F> y;
-        fe_mul(y, x, sc);
-        x = y;
-      }
+      // closing product: the scale (1/N) or internal one (R' mod p) maps the lazily
+      // grown value (< 33p) back below 2p, as fe_store_ref's canonicalisation needs
+      Fe<F> y;
+      fe_mul(y, x, sc);
+      x = y;
     }
     fe_store_ref(dst + addr * F::N64, x);
   }

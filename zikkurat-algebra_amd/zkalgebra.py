@@ -25,7 +25,8 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libzkalgebra_gpu.so")
+# ZK_LIB_PATH: A/B experiments with variant builds of the same library (default: in-tree build)
+LIB_PATH = os.environ.get("ZK_LIB_PATH") or os.path.join(HERE, "lib", "libzkalgebra_gpu.so")
 U64P = ctypes.POINTER(ctypes.c_uint64)
 
 CURVES = ("bn128", "bls12_381")

@@ -78,6 +78,93 @@ ZKG_API void bn128_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint6
 ZKG_API void bls12_381_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
 ZKG_API void bls12_381_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
 
+/* Fr vector operations around the NTT.  <C> in {bn128, bls12_381}.
+ *   lib/cbits/curves/array/mont/bls12_381_arr_mont.h:3-48 (bn128_arr_mont.h same lines),
+ *   bound by Haskell ZK.Algebra.Curves.<C>.Array (Array.hs:108-352).
+ *   n elements of Montgomery Fr (4 u64 each); coefficients are single elements.
+ *   inv / div follow the reference's batch inversion (Fr_mont.c:258-285): if ANY
+ *   (divisor) element is zero, EVERY output element is zero.  n == 0 is a no-op (the
+ *   reference asserts n >= 1 in batch_inv). */
+ZKG_API uint8_t bn128_arr_mont_is_valid ( int n, const uint64_t *src );
+ZKG_API uint8_t bn128_arr_mont_is_zero  ( int n, const uint64_t *src );
+ZKG_API uint8_t bn128_arr_mont_is_one   ( int n, const uint64_t *src );
+ZKG_API uint8_t bn128_arr_mont_is_equal ( int n, const uint64_t *src1, const uint64_t *src2 );
+ZKG_API void bn128_arr_mont_set_zero ( int n, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_set_one  ( int n, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_set_const( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_copy     ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_from_std ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_to_std   ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_append( int n1, int n2, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_neg ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_add ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_sub ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_sqr ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_mul ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_inv ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_div ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_neg_inplace ( int n, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_add_inplace ( int n, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bn128_arr_mont_sub_inplace ( int n, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bn128_arr_mont_sqr_inplace ( int n, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_mul_inplace ( int n, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bn128_arr_mont_inv_inplace ( int n, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_div_inplace ( int n, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bn128_arr_mont_sub_inplace_reverse ( int n, uint64_t *tgt, const uint64_t *src1 );
+ZKG_API void bn128_arr_mont_mul_add ( int n, const uint64_t *src1, const uint64_t *src2, const uint64_t *src3, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_mul_sub ( int n, const uint64_t *src1, const uint64_t *src2, const uint64_t *src3, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_dot_prod ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_powers ( int n, const uint64_t *coeffA, const uint64_t *coeffB, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_scale ( int n, const uint64_t *coeff, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_scale_inplace ( int n, const uint64_t *coeff, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_Ax_plus_y ( int n, const uint64_t *coeffA, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_Ax_plus_y_inplace ( int n, const uint64_t *coeffA, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bn128_arr_mont_Ax_plus_By ( int n, const uint64_t *coeffA, const uint64_t *coeffB, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bn128_arr_mont_Ax_plus_By_inplace ( int n, const uint64_t *coeffA, const uint64_t *coeffB, uint64_t *tgt, const uint64_t *src2 );
+/* division by the vanishing polynomial x^expo_n - eta (bls12_381_poly_mont.c:317-413) */
+ZKG_API void bn128_poly_mont_div_by_vanishing ( int n1, const uint64_t *src1, int expo_n, const uint64_t *eta, int nquot, uint64_t *quot, int nrem, uint64_t *rem );
+ZKG_API uint8_t bn128_poly_mont_quot_by_vanishing( int n1, const uint64_t *src1, int expo_n, const uint64_t *eta, int nquot, uint64_t *quot );
+
+ZKG_API uint8_t bls12_381_arr_mont_is_valid ( int n, const uint64_t *src );
+ZKG_API uint8_t bls12_381_arr_mont_is_zero  ( int n, const uint64_t *src );
+ZKG_API uint8_t bls12_381_arr_mont_is_one   ( int n, const uint64_t *src );
+ZKG_API uint8_t bls12_381_arr_mont_is_equal ( int n, const uint64_t *src1, const uint64_t *src2 );
+ZKG_API void bls12_381_arr_mont_set_zero ( int n, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_set_one  ( int n, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_set_const( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_copy     ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_from_std ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_to_std   ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_append( int n1, int n2, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_neg ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_add ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_sub ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_sqr ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_mul ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_inv ( int n, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_div ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_neg_inplace ( int n, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_add_inplace ( int n, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bls12_381_arr_mont_sub_inplace ( int n, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bls12_381_arr_mont_sqr_inplace ( int n, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_mul_inplace ( int n, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bls12_381_arr_mont_inv_inplace ( int n, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_div_inplace ( int n, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bls12_381_arr_mont_sub_inplace_reverse ( int n, uint64_t *tgt, const uint64_t *src1 );
+ZKG_API void bls12_381_arr_mont_mul_add ( int n, const uint64_t *src1, const uint64_t *src2, const uint64_t *src3, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_mul_sub ( int n, const uint64_t *src1, const uint64_t *src2, const uint64_t *src3, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_dot_prod ( int n, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_powers ( int n, const uint64_t *coeffA, const uint64_t *coeffB, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_scale ( int n, const uint64_t *coeff, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_scale_inplace ( int n, const uint64_t *coeff, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_Ax_plus_y ( int n, const uint64_t *coeffA, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_Ax_plus_y_inplace ( int n, const uint64_t *coeffA, uint64_t *tgt, const uint64_t *src2 );
+ZKG_API void bls12_381_arr_mont_Ax_plus_By ( int n, const uint64_t *coeffA, const uint64_t *coeffB, const uint64_t *src1, const uint64_t *src2, uint64_t *tgt );
+ZKG_API void bls12_381_arr_mont_Ax_plus_By_inplace ( int n, const uint64_t *coeffA, const uint64_t *coeffB, uint64_t *tgt, const uint64_t *src2 );
+/* division by the vanishing polynomial x^expo_n - eta (bls12_381_poly_mont.c:317-413) */
+ZKG_API void bls12_381_poly_mont_div_by_vanishing ( int n1, const uint64_t *src1, int expo_n, const uint64_t *eta, int nquot, uint64_t *quot, int nrem, uint64_t *rem );
+ZKG_API uint8_t bls12_381_poly_mont_quot_by_vanishing( int n1, const uint64_t *src1, int expo_n, const uint64_t *eta, int nquot, uint64_t *quot );
+
 /* ------------------------------------------------------------------------------
  * Part 2: extensions (not in the reference).  curve: 0 = bn128, 1 = bls12_381.
  * ---------------------------------------------------------------------------- */
@@ -99,6 +186,18 @@ ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, 
                                const uint64_t *d_grps, uint64_t *tgt_proj, int window_size);
 /* device-resident NTT: d_src / d_tgt DEVICE pointers; gen on the host */
 ZKG_API void zkg_ntt_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src, uint64_t *d_tgt);
+
+/* device-resident Fr vector ops: d_* are DEVICE pointers, kA/kB and dot's tgt HOST.
+ * op codes: 0 neg, 1 add, 2 sub, 3 sub_rev (b - a), 4 sqr, 5 mul, 6 mul_add, 7 mul_sub,
+ * 8 scale (kA a), 9 Ax_plus_y, 10 Ax_plus_By, 11 from_std, 12 to_std, 13 copy,
+ * 14 set_const (kA), 15 inv, 16 div (a / b) */
+ZKG_API void zkg_arr_op_device(int curve, int op, int n, const uint64_t *d_a, const uint64_t *d_b,
+                               const uint64_t *d_c, const uint64_t *kA, const uint64_t *kB, uint64_t *d_tgt);
+ZKG_API void zkg_arr_dot_device(int curve, int n, const uint64_t *d_a, const uint64_t *d_b, uint64_t *tgt);
+ZKG_API void zkg_arr_powers_device(int curve, int n, const uint64_t *kA, const uint64_t *kB, uint64_t *d_tgt);
+ZKG_API int zkg_poly_div_by_vanishing_device(int curve, int n1, const uint64_t *d_src, int expo_n,
+                                             const uint64_t *eta, int nquot, uint64_t *d_quot, int nrem,
+                                             uint64_t *d_rem);
 
 /* host helpers on G1 (projective, reference Montgomery form) */
 ZKG_API void zkg_g1_proj_add(int curve, const uint64_t *a, const uint64_t *b, uint64_t *out);

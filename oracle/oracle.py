@@ -105,6 +105,39 @@ class Oracle:
                                    ctypes.c_int64(count), _p(out))
         return out
 
+    ARR_OP = {"neg": 0, "add": 1, "sub": 2, "sub_rev": 3, "sqr": 4, "mul": 5, "mul_add": 6, "mul_sub": 7,
+              "scale": 8, "Ax_plus_y": 9, "Ax_plus_By": 10, "from_std": 11, "to_std": 12, "copy": 13,
+              "set_const": 14, "inv": 15, "div": 16}
+
+    def arr_op(self, curve, op, n, a=None, b=None, c=None, kA=None, kB=None):
+        out = np.zeros((n, 4), dtype=np.uint64)
+        z = np.zeros((max(n, 1), 4), dtype=np.uint64)
+        k0 = np.zeros(4, dtype=np.uint64)
+        arg = lambda x, d: _p(np.ascontiguousarray(x if x is not None else d, dtype=np.uint64))
+        self.lib.zko_arr_op(self._c(curve), self.ARR_OP[op], n, arg(a, z), arg(b, z), arg(c, z), arg(kA, k0),
+                            arg(kB, k0), _p(out))
+        return out
+
+    def arr_dot(self, curve, a, b):
+        out = np.zeros(4, dtype=np.uint64)
+        self.lib.zko_arr_dot(self._c(curve), a.shape[0], _p(a), _p(b), _p(out))
+        return out
+
+    def arr_powers(self, curve, kA, kB, n):
+        out = np.zeros((n, 4), dtype=np.uint64)
+        self.lib.zko_arr_powers(self._c(curve), n, _p(np.ascontiguousarray(kA)), _p(np.ascontiguousarray(kB)),
+                                _p(out))
+        return out
+
+    def div_by_vanishing(self, curve, poly, n, eta):
+        n1 = poly.shape[0]
+        nq, nr = max(0, n1 - n), max(0, n)
+        q = np.zeros((max(nq, 1), 4), dtype=np.uint64)
+        r = np.zeros((max(nr, 1), 4), dtype=np.uint64)
+        ok = self.lib.zko_div_by_vanishing(self._c(curve), n1, _p(poly), n, _p(np.ascontiguousarray(eta)), nq,
+                                           _p(q), nr, _p(r))
+        return q[:nq], r[:nr], bool(ok)
+
     def fft_generator(self, curve, m):
         out = np.zeros(4, dtype=np.uint64)
         self.lib.zko_fft_generator(self._c(curve), m, _p(out))
@@ -161,3 +194,11 @@ class Reference:
         out = np.zeros(3 * NP[curve], dtype=np.uint64)
         getattr(self.lib, f"{curve}_G1_proj_normalize")(_p(np.ascontiguousarray(proj)), _p(out))
         return out
+
+    def arr(self, curve, name, *args, restype=None):
+        """call <curve>_arr_mont_<name> / <curve>_poly_mont_<name> with numpy / int arguments"""
+        f = getattr(self.lib, f"{curve}_{name}")
+        if restype is not None:
+            f.restype = restype
+        conv = [_p(np.ascontiguousarray(a)) if isinstance(a, np.ndarray) else a for a in args]
+        return f(*conv)

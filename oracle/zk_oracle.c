@@ -678,3 +678,133 @@ void zko_fft_generator(int curve, int m, uint64_t *out) {
   for (int i = m; i < C->fftlog; i++) f_mul(Fr, g, g, g);
   memcpy(out, g, 8 * (size_t)Fr->n);
 }
+
+/* ==========================================================================
+ * Fr vector operations (lib/cbits/curves/array/mont/bls12_381_arr_mont.c) and
+ * division by a vanishing polynomial (lib/cbits/curves/poly/mont/bls12_381_poly_mont.c).
+ * Op codes = zikkurat-algebra_amd/csrc/zk_arr.hpp ArrOp. */
+#define FR_OF(c) (&FLD[CRV[c].fr])
+#define EL(p, i) ((p) + 4 * (size_t)(i))
+
+/* Fr_mont_batch_inv (bls12_381_Fr_mont.c:258-285): prefix products, one inversion,
+   backward sweep -- a zero anywhere makes every output zero */
+static void batch_inv(const fld_t *F, int n, const uint64_t *src, uint64_t *tgt) {
+  if (n <= 0) return;
+  uint64_t *prods = malloc(32 * (size_t)n), *recips = malloc(32 * (size_t)n);
+  memcpy(EL(prods, 0), EL(src, 0), 32);
+  for (int i = 1; i < n; i++) f_mul(F, EL(prods, i - 1), EL(src, i), EL(prods, i));
+  f_inv(F, EL(prods, n - 1), EL(recips, n - 1));
+  for (int i = n - 2; i >= 0; i--) f_mul(F, EL(recips, i + 1), EL(src, i + 1), EL(recips, i));
+  uint64_t first[4];
+  memcpy(first, EL(recips, 0), 32);
+  for (int i = n - 1; i >= 1; i--) f_mul(F, EL(recips, i), EL(prods, i - 1), EL(tgt, i));
+  memcpy(EL(tgt, 0), first, 32);
+  free(prods);
+  free(recips);
+}
+
+void zko_arr_op(int curve, int op, int n, const uint64_t *a, const uint64_t *b, const uint64_t *c,
+                const uint64_t *kA, const uint64_t *kB, uint64_t *tgt) {
+  zko_init();
+  const fld_t *F = FR_OF(curve);
+  if (op == 15 || op == 16) { /* inv / div (arr_mont.c: inv, div) */
+    if (n <= 0) return;
+    uint64_t *tmp = malloc(32 * (size_t)n);
+    batch_inv(F, n, op == 15 ? a : b, tmp);
+    for (int i = 0; i < n; i++) {
+      if (op == 15) memcpy(EL(tgt, i), EL(tmp, i), 32);
+      else f_mul(F, EL(a, i), EL(tmp, i), EL(tgt, i));
+    }
+    free(tmp);
+    return;
+  }
+  for (int i = 0; i < n; i++) {
+    uint64_t t[4], u[4];
+    switch (op) {
+      case 0: f_neg(F, EL(a, i), t); break;
+      case 1: f_add(F, EL(a, i), EL(b, i), t); break;
+      case 2: f_sub(F, EL(a, i), EL(b, i), t); break;
+      case 3: f_sub(F, EL(b, i), EL(a, i), t); break;                 /* sub_inplace_reverse */
+      case 4: f_mul(F, EL(a, i), EL(a, i), t); break;
+      case 5: f_mul(F, EL(a, i), EL(b, i), t); break;
+      case 6: f_mul(F, EL(a, i), EL(b, i), u); f_add(F, u, EL(c, i), t); break;  /* mul_add */
+      case 7: f_mul(F, EL(a, i), EL(b, i), u); f_sub(F, u, EL(c, i), t); break;  /* mul_sub */
+      case 8: f_mul(F, kA, EL(a, i), t); break;                        /* scale */
+      case 9: f_mul(F, kA, EL(a, i), u); f_add(F, u, EL(b, i), t); break;        /* Ax_plus_y */
+      case 10: {                                                       /* Ax_plus_By */
+        uint64_t v[4];
+        f_mul(F, kA, EL(a, i), u);
+        f_mul(F, kB, EL(b, i), v);
+        f_add(F, u, v, t);
+        break;
+      }
+      case 11: f_from_std(F, EL(a, i), t); break;
+      case 12: f_to_std(F, EL(a, i), t); break;
+      case 13: memcpy(t, EL(a, i), 32); break;
+      default: memcpy(t, kA, 32); break;                               /* set_const */
+    }
+    memcpy(EL(tgt, i), t, 32);
+  }
+}
+
+void zko_arr_dot(int curve, int n, const uint64_t *a, const uint64_t *b, uint64_t *tgt) {
+  zko_init();
+  const fld_t *F = FR_OF(curve);
+  uint64_t acc[4] = {0}, t[4];
+  for (int i = 0; i < n; i++) {
+    f_mul(F, EL(a, i), EL(b, i), t);
+    f_add(F, acc, t, acc);
+  }
+  memcpy(tgt, acc, 32);
+}
+
+void zko_arr_powers(int curve, int n, const uint64_t *kA, const uint64_t *kB, uint64_t *tgt) {
+  zko_init();
+  const fld_t *F = FR_OF(curve);
+  if (n <= 0) return;
+  memcpy(EL(tgt, 0), kA, 32);
+  for (int i = 1; i < n; i++) f_mul(F, EL(tgt, i - 1), kB, EL(tgt, i));
+}
+
+/* poly_mont_div_by_vanishing (bls12_381_poly_mont.c:317-397): quotient / remainder of
+   p(x) by x^n - eta; returns 1 if the remainder is zero (quot_by_vanishing, :402-413) */
+int zko_div_by_vanishing(int curve, int n1, const uint64_t *src, int n, const uint64_t *eta, int nquot,
+                         uint64_t *quot, int nrem, uint64_t *rem) {
+  zko_init();
+  const fld_t *F = FR_OF(curve);
+  int deg = -1;
+  for (int i = n1 - 1; i >= 0; i--)
+    if (!big_is_zero(EL(src, i), 4)) { deg = i; break; }
+  memset(quot, 0, 32 * (size_t)(nquot > 0 ? nquot : 0));
+  if (rem) memset(rem, 0, 32 * (size_t)(nrem > 0 ? nrem : 0));
+  uint64_t *r = rem;
+  uint64_t *tmp = NULL;
+  if (!r) { tmp = calloc((size_t)n, 32); r = tmp; }
+  if (deg < n) {
+    if (deg >= 0) memcpy(r, src, 32 * (size_t)(deg + 1));
+  } else {
+    for (int j = deg - n; j >= 0; j--) {
+      if (j + n <= deg - n) {
+        uint64_t t[4];
+        f_mul(F, EL(quot, j + n), eta, t);
+        f_add(F, EL(src, j + n), t, EL(quot, j));
+      } else {
+        memcpy(EL(quot, j), EL(src, j + n), 32);
+      }
+    }
+    for (int j = 0; j < n; j++) {
+      if (j <= deg - n) {
+        uint64_t t[4];
+        f_mul(F, EL(quot, j), eta, t);
+        f_add(F, EL(src, j), t, EL(r, j));
+      } else {
+        memcpy(EL(r, j), EL(src, j), 32);
+      }
+    }
+  }
+  int ok = 1;
+  for (int j = 0; j < n; j++)
+    if (!big_is_zero(EL(r, j), 4)) { ok = 0; break; }
+  free(tmp);
+  return ok;
+}

@@ -52,4 +52,14 @@ void zko_gen_fr(int curve, uint64_t seed, int64_t start, int64_t count, uint64_t
 void zko_gen_g1_points(int curve, uint64_t seed, int64_t start, int64_t count, uint64_t *out);
 void zko_fft_generator(int curve, int m, uint64_t *out);
 
+/* Fr vector ops (lib/cbits/curves/array/mont/bls12_381_arr_mont.c); op codes of
+ * zikkurat-algebra_amd/csrc/zk_arr.hpp (0 neg .. 16 div) */
+void zko_arr_op(int curve, int op, int n, const uint64_t *a, const uint64_t *b, const uint64_t *c,
+                const uint64_t *kA, const uint64_t *kB, uint64_t *tgt);
+void zko_arr_dot(int curve, int n, const uint64_t *a, const uint64_t *b, uint64_t *tgt);
+void zko_arr_powers(int curve, int n, const uint64_t *kA, const uint64_t *kB, uint64_t *tgt);
+/* bls12_381_poly_mont.c:317-413; rem may be NULL; returns 1 if the remainder is zero */
+int zko_div_by_vanishing(int curve, int n1, const uint64_t *src, int n, const uint64_t *eta, int nquot,
+                         uint64_t *quot, int nrem, uint64_t *rem);
+
 #endif

@@ -54,12 +54,13 @@ def test_reference_signatures_match_reference_headers():
     for c in ("bn128", "bls12_381"):
         for hdr, pat in ((f"g1/proj/{c}_G1_proj.h", r"MSM_(mont|std)_coeff_(proj|affine)_out(_variable)?\("),
                          (f"g1/jac/{c}_G1_jac.h", r"MSM_(mont|std)_coeff_(jac|affine)_out\("),
-                         (f"poly/mont/{c}_poly_mont.h", r"ntt_(forward|inverse)\(")):
+                         (f"poly/mont/{c}_poly_mont.h", r"ntt_(forward|inverse)\(|_by_vanishing\s*\("),
+                         (f"array/mont/{c}_arr_mont.h", r"_arr_mont_\w+\s*\(")):
             for line in open(os.path.join(ref, hdr)):
                 if re.search(pat, line) and "slow_reference" not in line and "noalloc" not in line:
                     proto = line.replace("extern", "").strip().rstrip(";")
                     name = re.search(r"(\w+)\s*\(", proto).group(1)
-                    ours_line = [l for l in ours.splitlines() if re.search(r"\b" + name + r"\(", l)]
+                    ours_line = [l for l in ours.splitlines() if re.search(r"\b" + name + r"\s*\(", l)]
                     assert ours_line, name
                     # compare parameter types only (names may differ)
                     ptypes = lambda s: [re.sub(r"\w+$", "", a.strip()).replace(" ", "")

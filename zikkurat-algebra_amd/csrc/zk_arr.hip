@@ -1,0 +1,642 @@
+// zk_arr.hip -- Fr vector operations and division by a vanishing polynomial on gfx950.
+//
+// Replaces the reference's generated vector code that sits between NTTs in a prover
+// (SURVEY.md 8f row 4):
+//   <C>_arr_mont_{neg,add,sub,sqr,mul,inv,div}[_inplace], _sub_inplace_reverse,
+//   _mul_add, _mul_sub, _scale[_inplace], _Ax_plus_y[_inplace], _Ax_plus_By[_inplace],
+//   _from_std, _to_std, _copy, _set_*, _append, _dot_prod, _powers, _is_*
+//        lib/cbits/curves/array/mont/bls12_381_arr_mont.c (bn128_arr_mont.c same layout)
+//   <C>_Fr_mont_batch_inv                         bls12_381_Fr_mont.c:258-285
+//   <C>_poly_mont_div_by_vanishing / _quot_by_vanishing / _degree
+//        lib/cbits/curves/poly/mont/bls12_381_poly_mont.c:26-32, 317-413
+//
+// Every result is the canonical Montgomery representative, so any exact schedule is
+// bit-identical to the reference's sequential loops; the reference's corner cases are
+// kept: batch inversion maps EVERY output to 0 when any input is 0 (its prefix-product
+// trick degenerates that way, Fr_mont.c:266-281), inv(0) = 0.
+//
+// Representation: values are loaded in the reference form x*R (R = 2^256) into the
+// device's unsaturated limbs (zk_field.hpp).  A product of two reference-form values
+// gives x y R^2 / R'; one more product by KIN = R'^2/R (fe_to_int) returns x y R.  A
+// coefficient used for a whole array is converted once (kA -> kA*R'), after which a
+// single product per element yields reference form directly.
+//
+// Roofline: element-wise ops move 32 B per operand and per result (HBM-bound at
+// 2^24 elements: a product costs ~170 mads, the VALU sustains ~1.5e11 Fr products/s,
+// i.e. ~2 products per 64 B of traffic at 8 TB/s).  Batch inversion is a chunked
+// Montgomery trick: CHK consecutive elements per lane, one Fermat inversion per chunk.
+#include <hipcub/hipcub.hpp>
+#include "zk_field.hpp"
+#include "zk_host.hpp"
+#include "zk_runtime.hpp"
+#include "zk_arr.hpp"
+
+namespace zk {
+
+struct U256 {
+  uint64_t w[4];
+};
+
+struct ArrArgs {
+  int op, n;
+  const uint64_t *a, *b, *c;
+  uint64_t *tgt;
+  U256 kA, kB;   // coefficients (reference form)
+  U256 cstd;     // R * R' mod p: from_std constant (x -> x R in one product)
+};
+
+template <class F>
+__device__ __forceinline__ void ld(Fe<F> &x, const uint64_t *p, size_t i) { fe_load_ref(x, p + i * 4); }
+template <class F>
+__device__ __forceinline__ void st(uint64_t *p, size_t i, const Fe<F> &x) { fe_store_ref(p + i * 4, x); }
+template <class F>
+__device__ __forceinline__ void ld_const(Fe<F> &x, const U256 &k) {
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    w[2 * j] = (uint32_t)k.w[j];
+    w[2 * j + 1] = (uint32_t)(k.w[j] >> 32);
+  }
+  fe_unpack(x, w);
+}
+// reference-form product: (xR)(yR) -> xyR
+template <class F>
+__device__ __forceinline__ void mul_ref(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  Fe<F> t;
+  fe_mul(t, a, b);
+  fe_to_int(r, t);
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_arr_map(ArrArgs g) {
+  Fe<F> kA, kB, cs;
+  if (g.op == ARR_SCALE || g.op == ARR_AXPY || g.op == ARR_AXPBY || g.op == ARR_SET_CONST) {
+    Fe<F> t;
+    ld_const(t, g.kA);
+    if (g.op == ARR_SET_CONST) kA = t; else fe_to_int(kA, t);
+  }
+  if (g.op == ARR_AXPBY) {
+    Fe<F> t;
+    ld_const(t, g.kB);
+    fe_to_int(kB, t);
+  }
+  if (g.op == ARR_FROM_STD) ld_const(cs, g.cstd);
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)g.n; i += stride) {
+    Fe<F> x, y, z, r;
+    switch (g.op) {
+      case ARR_NEG: ld(x, g.a, i); fe_neg(r, x); break;
+      case ARR_ADD: ld(x, g.a, i); ld(y, g.b, i); fe_add(r, x, y); break;
+      case ARR_SUB: ld(x, g.a, i); ld(y, g.b, i); fe_sub(r, x, y); break;
+      case ARR_SUB_REV: ld(x, g.a, i); ld(y, g.b, i); fe_sub(r, y, x); break;
+      case ARR_SQR: ld(x, g.a, i); fe_sqr(z, x); fe_to_int(r, z); break;
+      case ARR_MUL: ld(x, g.a, i); ld(y, g.b, i); mul_ref(r, x, y); break;
+      case ARR_MUL_ADD: ld(x, g.a, i); ld(y, g.b, i); mul_ref(z, x, y); ld(y, g.c, i); fe_add(r, z, y); break;
+      case ARR_MUL_SUB: ld(x, g.a, i); ld(y, g.b, i); mul_ref(z, x, y); ld(y, g.c, i); fe_sub(r, z, y); break;
+      case ARR_SCALE: ld(x, g.a, i); fe_mul(r, kA, x); break;
+      case ARR_AXPY: ld(x, g.a, i); fe_mul(z, kA, x); ld(y, g.b, i); fe_add(r, z, y); break;
+      case ARR_AXPBY: ld(x, g.a, i); fe_mul(z, kA, x); ld(y, g.b, i); fe_mul(x, kB, y); fe_add(r, z, x); break;
+      case ARR_FROM_STD: ld(x, g.a, i); fe_mul(r, x, cs); break;
+      case ARR_TO_STD: ld(x, g.a, i); fe_ref_to_std(r, x); break;
+      case ARR_COPY: ld(r, g.a, i); break;
+      default: r = kA; break;  // ARR_SET_CONST
+    }
+    st(g.tgt, i, r);
+  }
+}
+
+// ---------------------------------------------------------------------------- inversion
+
+// x^e (internal form), e = 256-bit exponent, square-and-multiply MSB first (the
+// exponent is the same for every lane: no divergence)
+template <class F>
+__device__ __forceinline__ void fe_pow_int(Fe<F> &r, const Fe<F> &x, const U256 &e) {
+  Fe<F> acc;
+  fe_one(acc);
+  for (int w = 3; w >= 0; w--) {
+    const uint64_t ew = e.w[w];
+    for (int b = 63; b >= 0; b--) {
+      Fe<F> t;
+      fe_sqr(t, acc);
+      acc = t;
+      if ((ew >> b) & 1) {
+        fe_mul(t, acc, x);
+        acc = t;
+      }
+    }
+  }
+  r = acc;
+}
+
+// Chunked Montgomery trick: lane t owns elements [t*CHK, (t+1)*CHK).  Pass 1 stores the
+// running prefix products (internal form, packed) in `scratch`; one Fermat inversion of
+// the chunk product; the backward pass emits 1/x_i (ARR_INV) or a_i / x_i (ARR_DIV, with
+// x = b).  Any zero x raises *zflag (the final kernel then zeroes everything).
+template <class F>
+__global__ void __launch_bounds__(256) k_inv_chunks(int op, int n, int CHK, const uint64_t *__restrict__ a,
+                                                    const uint64_t *__restrict__ x, uint64_t *__restrict__ scratch,
+                                                    uint64_t *tgt, U256 pm2, uint32_t *zflag) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i0 = t * CHK;
+  if (i0 >= (size_t)n) return;
+  const size_t i1 = min((size_t)n, i0 + CHK);
+  Fe<F> P;
+  fe_one(P);
+  bool zero = false;
+  for (size_t i = i0; i < i1; i++) {
+    Fe<F> v, vi, q;
+    ld(v, x, i);
+    zero |= fe_is_zero(v);
+    fe_to_int(vi, v);
+    fe_mul(q, P, vi);
+    P = q;
+    st(scratch, i, P);
+  }
+  if (zero) atomicOr(zflag, 1u);
+  Fe<F> inv;
+  fe_pow_int(inv, P, pm2);  // (prod)^-1, internal form
+  for (size_t i = i1; i-- > i0;) {
+    Fe<F> prev, out, v, vi, q;
+    if (i > i0) ld(prev, scratch, i - 1); else fe_one(prev);
+    fe_mul(out, inv, prev);  // 1/x_i (internal)
+    ld(v, x, i);
+    fe_to_int(vi, v);
+    fe_mul(q, inv, vi);
+    inv = q;
+    if (op == ARR_DIV) {
+      Fe<F> ai, r;
+      ld(ai, a, i);
+      fe_mul(r, out, ai);  // (1/x) R' * a R / R' = (a/x) R
+      st(tgt, i, r);
+    } else {
+      Fe<F> r;
+      fe_to_ref(r, out);
+      st(tgt, i, r);
+    }
+  }
+}
+
+__global__ void k_zero_if_flag(int n, uint64_t *__restrict__ tgt, const uint32_t *__restrict__ zflag) {
+  if (*zflag == 0) return;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n * 4; i += stride) tgt[i] = 0;
+}
+
+// ---------------------------------------------------------------------------- predicates
+
+__global__ void k_pred(int pred, int n, const uint64_t *__restrict__ a, const uint64_t *__restrict__ b, U256 prime,
+                       U256 one, uint32_t *__restrict__ fail) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += stride) {
+    const uint64_t *x = a + i * 4;
+    switch (pred) {
+      case PRED_IS_VALID: {  // x < p, Fr_mont.c:288-298
+        bool lt = false, decided = false;
+        for (int j = 3; j >= 0 && !decided; j--) {
+          if (x[j] != prime.w[j]) { lt = x[j] < prime.w[j]; decided = true; }
+        }
+        bad |= !lt;
+        break;
+      }
+      case PRED_IS_ZERO: bad |= (x[0] | x[1] | x[2] | x[3]) != 0; break;
+      case PRED_IS_ONE:
+        bad |= (x[0] != one.w[0]) | (x[1] != one.w[1]) | (x[2] != one.w[2]) | (x[3] != one.w[3]);
+        break;
+      default: {
+        const uint64_t *y = b + i * 4;
+        bad |= (x[0] != y[0]) | (x[1] != y[1]) | (x[2] != y[2]) | (x[3] != y[3]);
+      }
+    }
+  }
+  if (bad) atomicOr(fail, 1u);
+}
+
+// ---------------------------------------------------------------------------- dot product
+
+constexpr int DOT_THREADS = 256;
+template <class F>
+__global__ void __launch_bounds__(DOT_THREADS) k_dot(int n, const uint64_t *__restrict__ a,
+                                                     const uint64_t *__restrict__ b, uint64_t *__restrict__ part) {
+  __shared__ uint32_t lds[DOT_THREADS * F::N];
+  Fe<F> acc;
+  fe_zero(acc);
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += stride) {
+    Fe<F> x, y, z, s;
+    ld(x, a, i);
+    ld(y, b, i);
+    fe_mul(z, x, y);  // x y R^2 / R' (converted once, after the sum)
+    fe_add(s, acc, z);
+    acc = s;
+  }
+  for (int q = 0; q < F::N; q++) lds[threadIdx.x * F::N + q] = acc.v[q];
+  __syncthreads();
+  for (int s = DOT_THREADS / 2; s >= 1; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      Fe<F> o, r;
+      for (int q = 0; q < F::N; q++) o.v[q] = lds[(threadIdx.x + s) * F::N + q];
+      fe_add(r, acc, o);
+      acc = r;
+      for (int q = 0; q < F::N; q++) lds[threadIdx.x * F::N + q] = acc.v[q];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) st(part, blockIdx.x, acc);  // canonical, still in the R^2/R' form
+}
+template <class F>
+__global__ void k_dot_final(int nparts, const uint64_t *__restrict__ part, uint64_t *__restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Fe<F> acc;
+  fe_zero(acc);
+  for (int i = 0; i < nparts; i++) {
+    Fe<F> x, s;
+    ld(x, part, i);
+    fe_add(s, acc, x);
+    acc = s;
+  }
+  Fe<F> r;
+  fe_to_int(r, acc);  // x y R^2/R' * R'^2/R / R' = x y R
+  st(out, 0, r);
+}
+
+// ---------------------------------------------------------------------------- powers
+
+// tlo[i] = B^i (internal, i < 2^h);  thi[j] = A * B^(j 2^h) (reference form)
+template <class F>
+__global__ void k_pow_tables(int h, int nlo, int nhi, U256 kA, U256 kB, uint64_t *__restrict__ tlo,
+                             uint64_t *__restrict__ thi) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  Fe<F> Bref, B;
+  ld_const(Bref, kB);
+  fe_to_int(B, Bref);
+  if (i < nlo) {
+    Fe<F> acc, base = B, t;
+    fe_one(acc);
+    for (int e = i; e; e >>= 1) {
+      if (e & 1) { fe_mul(t, acc, base); acc = t; }
+      fe_sqr(t, base);
+      base = t;
+    }
+    st(tlo, i, acc);
+  }
+  if (i < nhi) {
+    Fe<F> base = B, t, acc;
+    for (int s = 0; s < h; s++) { fe_sqr(t, base); base = t; }  // B^(2^h)
+    ld_const(acc, kA);  // reference form A R
+    for (int e = i; e; e >>= 1) {
+      if (e & 1) { fe_mul(t, acc, base); acc = t; }
+      fe_sqr(t, base);
+      base = t;
+    }
+    st(thi, i, acc);
+  }
+}
+template <class F>
+__global__ void __launch_bounds__(256) k_powers(int n, int h, const uint64_t *__restrict__ tlo,
+                                                const uint64_t *__restrict__ thi, uint64_t *__restrict__ tgt) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += stride) {
+    Fe<F> lo, hi, r;
+    ld(lo, tlo, i & ((1u << h) - 1));
+    ld(hi, thi, i >> h);
+    fe_mul(r, hi, lo);  // A B^(j 2^h) R * B^l R' / R'
+    st(tgt, i, r);
+  }
+}
+
+// ---------------------------------------------------------------------------- vanishing
+
+__global__ void k_degree(int n, const uint64_t *__restrict__ a, int *__restrict__ deg) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  int best = -1;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += stride) {
+    const uint64_t *x = a + i * 4;
+    if (x[0] | x[1] | x[2] | x[3]) best = (int)i;
+  }
+  if (best >= 0) atomicMax(deg, best);
+}
+// quotient by x^n - eta (deg_p >= n): q_j = a_{j+n} + eta q_{j+n}, one lane per residue
+// class j mod n walking its chain from the top (poly_mont.c:360-372 / 337-347)
+template <class F>
+__global__ void __launch_bounds__(256) k_vanish_quot(int deg, int n, const uint64_t *__restrict__ a, U256 eta,
+                                                     uint64_t *__restrict__ quot) {
+  const int rho = blockIdx.x * blockDim.x + threadIdx.x;
+  const int top = deg - n;  // largest quotient index
+  if (rho >= n || rho > top) return;
+  Fe<F> e, er;
+  ld_const(er, eta);
+  fe_to_int(e, er);
+  Fe<F> q;
+  fe_zero(q);
+  const int jmax = rho + ((top - rho) / n) * n;
+  for (int j = jmax; j >= rho; j -= n) {
+    Fe<F> ai, t;
+    ld(ai, a, (size_t)j + n);
+    fe_mul(t, e, q);  // eta * q_{j+n} (0 at the top of the chain)
+    fe_add(q, ai, t);
+    st(quot, (size_t)j, q);
+  }
+}
+template <class F>
+__global__ void __launch_bounds__(256) k_vanish_rem(int deg, int n, const uint64_t *__restrict__ a,
+                                                    const uint64_t *__restrict__ quot, U256 eta,
+                                                    uint64_t *__restrict__ rem) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  Fe<F> aj, r;
+  ld(aj, a, j);
+  if (j <= deg - n) {
+    Fe<F> e, er, q, t;
+    ld_const(er, eta);
+    fe_to_int(e, er);
+    ld(q, quot, j);
+    fe_mul(t, e, q);
+    fe_add(r, aj, t);
+  } else {
+    r = aj;
+  }
+  st(rem, j, r);
+}
+
+// ---------------------------------------------------------------------------- host side
+
+struct CfgBN { using Fd = BN_Fr; using Fh = zkh::BN_Fr; };
+struct CfgBLS { using Fd = BLS_Fr; using Fh = zkh::BLS_Fr; };
+
+template <class Fh>
+static U256 to_u256(const zkh::Fe<Fh> &x) {
+  U256 u;
+  for (int j = 0; j < 4; j++) u.w[j] = x.v[j];
+  return u;
+}
+static U256 load_u256(const uint64_t *p) {
+  U256 u = {{0, 0, 0, 0}};
+  if (p) for (int j = 0; j < 4; j++) u.w[j] = p[j];
+  return u;
+}
+
+// R * R' mod p as a plain integer: R' = 2^(RB N) = R * 2^(RB N - 256), so R R' = R^2 2^d
+template <class Cfg>
+static U256 from_std_const() {
+  using Fh = typename Cfg::Fh;
+  using Fd = typename Cfg::Fd;
+  zkh::Fe<Fh> x;
+  memcpy(x.v, Fh::R2, sizeof x.v);
+  for (int d = 0; d < Fd::RB * Fd::N - 64 * Fh::N; d++) zkh::add(x, x, x);
+  return to_u256(x);
+}
+template <class Cfg>
+static U256 p_minus_2() {
+  using Fh = typename Cfg::Fh;
+  U256 e;
+  for (int j = 0; j < 4; j++) e.w[j] = Fh::P[j];
+  uint64_t br = 2;
+  for (int j = 0; j < 4 && br; j++) {
+    const uint64_t o = e.w[j];
+    e.w[j] = o - br;
+    br = o < br ? 1 : 0;
+  }
+  return e;
+}
+
+static unsigned grid_for(size_t n) {
+  size_t b = (n + 255) / 256;
+  if (b > 4096) b = 4096;  // grid-stride loops beyond ~16 waves per SIMD
+  return (unsigned)(b ? b : 1);
+}
+
+// staging of host operands: every array is copied into the call's arena
+struct Stage {
+  Device &dev;
+  bool host;
+  explicit Stage(Device &d, bool h) : dev(d), host(h) {}
+  const uint64_t *in(const uint64_t *p, size_t n) {
+    if (!host || !p) return p;
+    uint64_t *d = dev.arena.take<uint64_t>(n * 4);
+    if (n) ZK_CHECK(hipMemcpyAsync(d, p, n * 32, hipMemcpyHostToDevice, dev.stream));
+    return d;
+  }
+  uint64_t *out(uint64_t *p, size_t n) { return host ? dev.arena.take<uint64_t>(n * 4) : p; }
+  void back(uint64_t *host_p, const uint64_t *dev_p, size_t n) {
+    if (host && n) ZK_CHECK(hipMemcpyAsync(host_p, dev_p, n * 32, hipMemcpyDeviceToHost, dev.stream));
+  }
+};
+
+template <class Cfg>
+static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64_t *b, const uint64_t *c,
+                     const uint64_t *kA, const uint64_t *kB, uint64_t *tgt, bool host_io) {
+  using F = typename Cfg::Fd;
+  hipStream_t st = dev.stream;
+  const size_t N = (size_t)(n > 0 ? n : 0);
+  dev.arena.reserve(N * 32 * 5 + (1 << 20));
+  dev.arena.reset();
+  Stage sg(dev, host_io);
+  const bool needb = op == ARR_ADD || op == ARR_SUB || op == ARR_SUB_REV || op == ARR_MUL || op == ARR_MUL_ADD ||
+                     op == ARR_MUL_SUB || op == ARR_AXPY || op == ARR_AXPBY || op == ARR_DIV;
+  const bool needa = op != ARR_SET_CONST;
+  const uint64_t *da = needa ? sg.in(a, N) : nullptr;
+  const uint64_t *db = needb ? sg.in(b, N) : nullptr;
+  const uint64_t *dc = (op == ARR_MUL_ADD || op == ARR_MUL_SUB) ? sg.in(c, N) : nullptr;
+  uint64_t *dt = sg.out(tgt, N);
+  if (N) {
+    if (op == ARR_INV || op == ARR_DIV) {
+      const int CHK = 32;
+      uint64_t *scratch = dev.arena.take<uint64_t>(N * 4);
+      uint32_t *flag = dev.arena.take<uint32_t>(1);
+      ZK_CHECK(hipMemsetAsync(flag, 0, 4, st));
+      const size_t lanes = (N + CHK - 1) / CHK;
+      hipLaunchKernelGGL(k_inv_chunks<F>, dim3(div_up(lanes, 256)), dim3(256), 0, st, op, n, CHK, da,
+                         op == ARR_DIV ? db : da, scratch, dt, p_minus_2<Cfg>(), flag);
+      ZK_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(k_zero_if_flag, dim3(grid_for(N * 4)), dim3(256), 0, st, n, dt, flag);
+      ZK_CHECK(hipGetLastError());
+    } else {
+      ArrArgs g;
+      g.op = op;
+      g.n = n;
+      g.a = da;
+      g.b = db;
+      g.c = dc;
+      g.tgt = dt;
+      g.kA = load_u256(kA);
+      g.kB = load_u256(kB);
+      g.cstd = from_std_const<Cfg>();
+      hipLaunchKernelGGL(k_arr_map<F>, dim3(grid_for(N)), dim3(256), 0, st, g);
+      ZK_CHECK(hipGetLastError());
+    }
+  }
+  sg.back(tgt, dt, N);
+  ZK_CHECK(hipStreamSynchronize(st));
+}
+
+template <class Cfg>
+static int arr_pred_t(Device &dev, int pred, int n, const uint64_t *a, const uint64_t *b, bool host_io) {
+  using Fh = typename Cfg::Fh;
+  hipStream_t st = dev.stream;
+  const size_t N = (size_t)(n > 0 ? n : 0);
+  dev.arena.reserve(N * 32 * 2 + (1 << 20));
+  dev.arena.reset();
+  Stage sg(dev, host_io);
+  const uint64_t *da = sg.in(a, N);
+  const uint64_t *db = pred == PRED_IS_EQUAL ? sg.in(b, N) : nullptr;
+  uint32_t *fail = dev.arena.take<uint32_t>(1);
+  ZK_CHECK(hipMemsetAsync(fail, 0, 4, st));
+  U256 prime, one;
+  for (int j = 0; j < 4; j++) { prime.w[j] = Fh::P[j]; one.w[j] = Fh::ONE[j]; }
+  if (N) {
+    hipLaunchKernelGGL(k_pred, dim3(grid_for(N)), dim3(256), 0, st, pred, n, da, db, prime, one, fail);
+    ZK_CHECK(hipGetLastError());
+  }
+  uint32_t *h = reinterpret_cast<uint32_t *>(dev.host_staging(4));
+  ZK_CHECK(hipMemcpyAsync(h, fail, 4, hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+  return *h ? 0 : 1;
+}
+
+template <class Cfg>
+static void arr_dot_t(Device &dev, int n, const uint64_t *a, const uint64_t *b, uint64_t *tgt_host, bool host_io) {
+  using F = typename Cfg::Fd;
+  hipStream_t st = dev.stream;
+  const size_t N = (size_t)(n > 0 ? n : 0);
+  dev.arena.reserve(N * 32 * 2 + (1 << 20));
+  dev.arena.reset();
+  Stage sg(dev, host_io);
+  const uint64_t *da = sg.in(a, N), *db = sg.in(b, N);
+  unsigned blocks = grid_for(N);
+  if (blocks > 1024) blocks = 1024;
+  uint64_t *part = dev.arena.take<uint64_t>((size_t)blocks * 4);
+  uint64_t *out = dev.arena.take<uint64_t>(4);
+  hipLaunchKernelGGL(k_dot<F>, dim3(blocks), dim3(DOT_THREADS), 0, st, n, da, db, part);
+  ZK_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_dot_final<F>, dim3(1), dim3(64), 0, st, (int)blocks, part, out);
+  ZK_CHECK(hipGetLastError());
+  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(32));
+  ZK_CHECK(hipMemcpyAsync(h, out, 32, hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+  memcpy(tgt_host, h, 32);
+}
+
+template <class Cfg>
+static void arr_powers_t(Device &dev, int n, const uint64_t *kA, const uint64_t *kB, uint64_t *tgt, bool host_io) {
+  using F = typename Cfg::Fd;
+  hipStream_t st = dev.stream;
+  if (n <= 0) return;  // powers: n == 0 writes nothing (arr_mont.c)
+  const size_t N = (size_t)n;
+  int lg = 0;
+  while (((size_t)1 << lg) < N) lg++;
+  const int h = (lg + 1) / 2;
+  const int nlo = 1 << h, nhi = (int)((N + nlo - 1) >> h);
+  dev.arena.reserve(N * 32 + ((size_t)nlo + nhi) * 32 + (1 << 20));
+  dev.arena.reset();
+  Stage sg(dev, host_io);
+  uint64_t *dt = sg.out(tgt, N);
+  uint64_t *tlo = dev.arena.take<uint64_t>((size_t)nlo * 4);
+  uint64_t *thi = dev.arena.take<uint64_t>((size_t)nhi * 4);
+  const int nt = nlo > nhi ? nlo : nhi;
+  hipLaunchKernelGGL(k_pow_tables<F>, dim3(div_up(nt, 256)), dim3(256), 0, st, h, nlo, nhi, load_u256(kA),
+                     load_u256(kB), tlo, thi);
+  ZK_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_powers<F>, dim3(grid_for(N)), dim3(256), 0, st, n, h, tlo, thi, dt);
+  ZK_CHECK(hipGetLastError());
+  sg.back(tgt, dt, N);
+  ZK_CHECK(hipStreamSynchronize(st));
+}
+
+template <class Cfg>
+static int div_vanishing_t(Device &dev, int n1, const uint64_t *src, int n, const uint64_t *eta, int nquot,
+                           uint64_t *quot, int nrem, uint64_t *rem, bool host_io) {
+  hipStream_t st = dev.stream;
+  ZK_REQUIRE(n >= 1, "poly_div_by_vanishing: expo_n must be >= 1");  // poly_mont.c:330
+  ZK_REQUIRE(quot != nullptr, "poly_div_by_vanishing: quot cannot be NULL");  // poly_mont.c:327
+  const size_t N1 = (size_t)(n1 > 0 ? n1 : 0);
+  const bool want_rem = rem != nullptr;
+  const size_t NR = want_rem ? (size_t)nrem : (size_t)n;  // quot_by_vanishing: internal rem of n
+  dev.arena.reserve((N1 + (size_t)nquot + NR) * 32 + (1 << 20));
+  dev.arena.reset();
+  Stage sg(dev, host_io);
+  const uint64_t *da = sg.in(src, N1);
+  uint64_t *dq = sg.out(quot, (size_t)nquot);
+  uint64_t *dr = want_rem ? sg.out(rem, NR) : dev.arena.take<uint64_t>(NR * 4);
+  int *ddeg = dev.arena.take<int>(1);
+  ZK_CHECK(hipMemsetAsync(ddeg, 0xff, 4, st));  // -1
+  if (N1) {
+    hipLaunchKernelGGL(k_degree, dim3(grid_for(N1)), dim3(256), 0, st, n1, da, ddeg);
+    ZK_CHECK(hipGetLastError());
+  }
+  int *hdeg = reinterpret_cast<int *>(dev.host_staging(4));
+  ZK_CHECK(hipMemcpyAsync(hdeg, ddeg, 4, hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+  const int deg = *hdeg;
+  ZK_REQUIRE(nquot >= deg - n + 1, "poly_div_by_vanishing: quotient buffer too small");  // poly_mont.c:328
+  ZK_REQUIRE(!want_rem || nrem >= n, "poly_div_by_vanishing: remainder buffer too small");  // :329
+  if (nquot > 0) ZK_CHECK(hipMemsetAsync(dq, 0, (size_t)nquot * 32, st));
+  if (NR) ZK_CHECK(hipMemsetAsync(dr, 0, NR * 32, st));
+  const U256 e = load_u256(eta);
+  if (deg < n) {  // quotient 0, remainder = p (poly_mont.c:332-341)
+    if (deg >= 0) {
+      ZK_REQUIRE(NR >= (size_t)deg + 1, "poly_div_by_vanishing: remainder buffer too small");
+      ZK_CHECK(hipMemcpyAsync(dr, da, (size_t)(deg + 1) * 32, hipMemcpyDeviceToDevice, st));
+    }
+  } else {
+    using F = typename Cfg::Fd;
+    hipLaunchKernelGGL(k_vanish_quot<F>, dim3(div_up(n, 256)), dim3(256), 0, st, deg, n, da, e, dq);
+    ZK_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_vanish_rem<F>, dim3(div_up(n, 256)), dim3(256), 0, st, deg, n, da, dq, e, dr);
+    ZK_CHECK(hipGetLastError());
+  }
+  sg.back(quot, dq, (size_t)nquot);
+  if (want_rem) {
+    sg.back(rem, dr, NR);
+    ZK_CHECK(hipStreamSynchronize(st));
+    return -1;
+  }
+  // quot_by_vanishing: is the remainder (n coefficients) zero?
+  uint32_t *fail = dev.arena.take<uint32_t>(1);
+  ZK_CHECK(hipMemsetAsync(fail, 0, 4, st));
+  U256 z = {{0, 0, 0, 0}};
+  hipLaunchKernelGGL(k_pred, dim3(grid_for(NR)), dim3(256), 0, st, (int)PRED_IS_ZERO, (int)NR, dr, nullptr, z, z,
+                     fail);
+  ZK_CHECK(hipGetLastError());
+  uint32_t *h = reinterpret_cast<uint32_t *>(dev.host_staging(4));
+  ZK_CHECK(hipMemcpyAsync(h, fail, 4, hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+  return *h ? 0 : 1;
+}
+
+// ---------------------------------------------------------------------------- public
+
+void arr_op(int curve, int op, int n, const uint64_t *a, const uint64_t *b, const uint64_t *c, const uint64_t *kA,
+            const uint64_t *kB, uint64_t *tgt, bool host_io) {
+  ZK_REQUIRE(op >= 0 && op < ARR_NUM_OPS, "arr_op: unknown operation");
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  if (curve == 0) arr_op_t<CfgBN>(dev, op, n, a, b, c, kA, kB, tgt, host_io);
+  else arr_op_t<CfgBLS>(dev, op, n, a, b, c, kA, kB, tgt, host_io);
+}
+int arr_pred(int curve, int pred, int n, const uint64_t *a, const uint64_t *b, bool host_io) {
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  return curve == 0 ? arr_pred_t<CfgBN>(dev, pred, n, a, b, host_io) : arr_pred_t<CfgBLS>(dev, pred, n, a, b, host_io);
+}
+void arr_dot(int curve, int n, const uint64_t *a, const uint64_t *b, uint64_t *tgt_host, bool host_io) {
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  if (curve == 0) arr_dot_t<CfgBN>(dev, n, a, b, tgt_host, host_io);
+  else arr_dot_t<CfgBLS>(dev, n, a, b, tgt_host, host_io);
+}
+void arr_powers(int curve, int n, const uint64_t *kA, const uint64_t *kB, uint64_t *tgt, bool host_io) {
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  if (curve == 0) arr_powers_t<CfgBN>(dev, n, kA, kB, tgt, host_io);
+  else arr_powers_t<CfgBLS>(dev, n, kA, kB, tgt, host_io);
+}
+int poly_div_by_vanishing(int curve, int n1, const uint64_t *src, int expo_n, const uint64_t *eta, int nquot,
+                          uint64_t *quot, int nrem, uint64_t *rem, bool host_io) {
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  return curve == 0 ? div_vanishing_t<CfgBN>(dev, n1, src, expo_n, eta, nquot, quot, nrem, rem, host_io)
+                    : div_vanishing_t<CfgBLS>(dev, n1, src, expo_n, eta, nquot, quot, nrem, rem, host_io);
+}
+
+}  // namespace zk

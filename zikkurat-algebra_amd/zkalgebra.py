@@ -41,12 +41,21 @@ REFERENCE_SYMBOLS = [
 ] + [f"{c}_G1_proj_MSM_std_coeff_proj_out_variable" for c in CURVES] + [
     f"{c}_G1_jac_MSM_{k}_coeff_{o}_out" for c in CURVES for k in ("mont", "std") for o in ("jac", "affine")
 ] + [f"{c}_poly_mont_ntt_{d}" for c in CURVES for d in ("forward", "inverse")]
+# Fr vector ops (lib/cbits/curves/array/mont/<C>_arr_mont.h:3-48) + division by a vanishing polynomial
+ARR_OPS = ["is_valid", "is_zero", "is_one", "is_equal", "set_zero", "set_one", "set_const", "copy", "from_std",
+           "to_std", "append", "neg", "add", "sub", "sqr", "mul", "inv", "div", "neg_inplace", "add_inplace",
+           "sub_inplace", "sqr_inplace", "mul_inplace", "inv_inplace", "div_inplace", "sub_inplace_reverse",
+           "mul_add", "mul_sub", "dot_prod", "powers", "scale", "scale_inplace", "Ax_plus_y", "Ax_plus_y_inplace",
+           "Ax_plus_By", "Ax_plus_By_inplace"]
+REFERENCE_SYMBOLS += [f"{c}_arr_mont_{o}" for c in CURVES for o in ARR_OPS] + [
+    f"{c}_poly_mont_{k}_by_vanishing" for c in CURVES for k in ("div", "quot")]
 EXTENSION_SYMBOLS = [
     "zkg_version", "zkg_device_count", "zkg_set_device", "zkg_device_malloc", "zkg_device_free",
     "zkg_memcpy_htod", "zkg_memcpy_dtoh", "zkg_device_synchronize", "zkg_g1_msm_device", "zkg_ntt_device",
     "zkg_g1_proj_add", "zkg_g1_proj_normalize", "zkg_g1_proj_to_affine", "zkg_gen_fr", "zkg_gen_g1_points",
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
-    "zkg_field_mul_rate",
+    "zkg_field_mul_rate", "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
+    "zkg_poly_div_by_vanishing_device",
 ]
 
 _lib = None
@@ -74,6 +83,14 @@ def load():
         lib.zkg_timer_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]
         lib.zkg_field_mul_rate.restype = ctypes.c_double
         lib.zkg_field_mul_rate.argtypes = [ctypes.c_int]
+        for c in CURVES:
+            for o in ("is_valid", "is_zero", "is_one", "is_equal"):
+                getattr(lib, f"{c}_arr_mont_{o}").restype = ctypes.c_uint8
+            getattr(lib, f"{c}_poly_mont_quot_by_vanishing").restype = ctypes.c_uint8
+        lib.zkg_arr_op_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, U64P, U64P, ctypes.c_void_p]
+        lib.zkg_arr_dot_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, U64P]
+        lib.zkg_arr_powers_device.argtypes = [ctypes.c_int, ctypes.c_int, U64P, U64P, ctypes.c_void_p]
         _lib = lib
     return _lib
 
@@ -233,6 +250,173 @@ ntt = forward_ntt
 intt = inverse_ntt
 
 
+# ----------------------------------------------------------------------------- Fr vectors
+
+def _fr(a):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    if a.ndim != 2 or a.shape[1] != NLIMBS_R:
+        raise TypeError("FlatArray Fr must have shape (n, 4)")
+    return a
+
+
+def _same(name, *arrs):
+    if any(x.shape[0] != arrs[0].shape[0] for x in arrs):
+        raise ValueError(f"{name}: incompatible input array lengths")   # Array.hs:217-360
+
+
+def _arr(curve, op):
+    require_gpu()
+    return getattr(load(), f"{curve}_arr_mont_{op}")
+
+
+def arr_is_valid(curve, a):
+    a = _fr(a)
+    return bool(_arr(curve, "is_valid")(a.shape[0], _p(a)))
+
+
+def arr_is_zero(curve, a):
+    a = _fr(a)
+    return bool(_arr(curve, "is_zero")(a.shape[0], _p(a)))
+
+
+def arr_is_one(curve, a):
+    a = _fr(a)
+    return bool(_arr(curve, "is_one")(a.shape[0], _p(a)))
+
+
+def arr_is_equal(curve, a, b):
+    a, b = _fr(a), _fr(b)
+    _same("isEqual", a, b)
+    return bool(_arr(curve, "is_equal")(a.shape[0], _p(a), _p(b)))
+
+
+def _unary(curve, op, a):
+    a = _fr(a)
+    out = np.zeros_like(a)
+    _arr(curve, op)(a.shape[0], _p(a), _p(out))
+    return out
+
+
+def _binary(curve, op, name, a, b):
+    a, b = _fr(a), _fr(b)
+    _same(name, a, b)
+    out = np.zeros_like(a)
+    _arr(curve, op)(a.shape[0], _p(a), _p(b), _p(out))
+    return out
+
+
+def arr_from_std(curve, a): return _unary(curve, "from_std", a)
+def arr_to_std(curve, a): return _unary(curve, "to_std", a)
+def arr_neg(curve, a): return _unary(curve, "neg", a)
+def arr_sqr(curve, a): return _unary(curve, "sqr", a)
+def arr_inv(curve, a): return _unary(curve, "inv", a)
+def arr_add(curve, a, b): return _binary(curve, "add", "add", a, b)
+def arr_sub(curve, a, b): return _binary(curve, "sub", "sub", a, b)
+def arr_mul(curve, a, b): return _binary(curve, "mul", "mul", a, b)
+def arr_div(curve, a, b): return _binary(curve, "div", "div", a, b)
+
+
+def arr_append(curve, a, b):
+    a, b = _fr(a), _fr(b)
+    out = np.zeros((a.shape[0] + b.shape[0], 4), dtype=np.uint64)
+    _arr(curve, "append")(a.shape[0], b.shape[0], _p(a), _p(b), _p(out))
+    return out
+
+
+def arr_cons(curve, x, a): return arr_append(curve, np.asarray(x, dtype=np.uint64).reshape(1, 4), a)
+def arr_snoc(curve, a, y): return arr_append(curve, a, np.asarray(y, dtype=np.uint64).reshape(1, 4))
+
+
+def arr_scale(curve, k, a):
+    a = _fr(a)
+    out = np.zeros_like(a)
+    _arr(curve, "scale")(a.shape[0], _p(np.ascontiguousarray(k, dtype=np.uint64)), _p(a), _p(out))
+    return out
+
+
+def arr_dot_prod(curve, a, b):
+    a, b = _fr(a), _fr(b)
+    _same("dotProd", a, b)
+    out = np.zeros(4, dtype=np.uint64)
+    _arr(curve, "dot_prod")(a.shape[0], _p(a), _p(b), _p(out))
+    return out
+
+
+def arr_powers(curve, a, b, n):
+    """powers a b n = [a b^i | i <- [0..n-1]] (Array.hs:99)"""
+    out = np.zeros((n, 4), dtype=np.uint64)
+    _arr(curve, "powers")(n, _p(np.ascontiguousarray(a, dtype=np.uint64)),
+                          _p(np.ascontiguousarray(b, dtype=np.uint64)), _p(out))
+    return out
+
+
+def _fused(curve, op, name, a, b, c):
+    a, b, c = _fr(a), _fr(b), _fr(c)
+    _same(name, a, b, c)
+    out = np.zeros_like(a)
+    _arr(curve, op)(a.shape[0], _p(a), _p(b), _p(c), _p(out))
+    return out
+
+
+def arr_mul_add(curve, a, b, c): return _fused(curve, "mul_add", "mulAdd", a, b, c)
+def arr_mul_sub(curve, a, b, c): return _fused(curve, "mul_sub", "mulSub", a, b, c)
+
+
+def arr_lin_comb1(curve, ax, y):
+    """linComb1 (a, x) y = a x + y (Array.hs:135-146)"""
+    (a, x), y = ax, _fr(y)
+    x = _fr(x)
+    if x.shape[0] != y.shape[0]:
+        raise ValueError("linComb1: incompatible vector dimensions")
+    out = np.zeros_like(x)
+    _arr(curve, "Ax_plus_y")(x.shape[0], _p(np.ascontiguousarray(a, dtype=np.uint64)), _p(x), _p(y), _p(out))
+    return out
+
+
+def arr_lin_comb2(curve, ax, by):
+    """linComb2 (a, x) (b, y) = a x + b y (Array.hs:148-161)"""
+    (a, x), (b, y) = ax, by
+    x, y = _fr(x), _fr(y)
+    if x.shape[0] != y.shape[0]:
+        raise ValueError("linComb2: incompatible vector dimensions")
+    out = np.zeros_like(x)
+    _arr(curve, "Ax_plus_By")(x.shape[0], _p(np.ascontiguousarray(a, dtype=np.uint64)),
+                              _p(np.ascontiguousarray(b, dtype=np.uint64)), _p(x), _p(y), _p(out))
+    return out
+
+
+def div_by_vanishing(curve, poly, expo_n, eta):
+    """Poly.divByVanishing (Poly.hs:367-380): (quotient, remainder) by x^n - eta."""
+    poly = _fr(poly)
+    n1 = poly.shape[0]
+    nq, nr = max(0, n1 - expo_n), max(0, expo_n)
+    q = np.zeros((nq, 4), dtype=np.uint64)
+    r = np.zeros((nr, 4), dtype=np.uint64)
+    require_gpu()
+    getattr(load(), f"{curve}_poly_mont_div_by_vanishing")(n1, _p(poly), expo_n,
+                                                            _p(np.ascontiguousarray(eta, dtype=np.uint64)),
+                                                            nq, _p(q), nr, _p(r))
+    return q, r
+
+
+def quot_by_vanishing(curve, poly, expo_n, eta):
+    """Poly.quotByVanishing (Poly.hs:383-397): the quotient, or None if the remainder is nonzero."""
+    poly = _fr(poly)
+    n1 = poly.shape[0]
+    nq = max(0, n1 - expo_n)
+    q = np.zeros((nq, 4), dtype=np.uint64)
+    require_gpu()
+    ok = getattr(load(), f"{curve}_poly_mont_quot_by_vanishing")(n1, _p(poly), expo_n,
+                                                                  _p(np.ascontiguousarray(eta, dtype=np.uint64)),
+                                                                  nq, _p(q))
+    return q if ok else None
+
+
+ARR_OP_CODE = {"neg": 0, "add": 1, "sub": 2, "sub_rev": 3, "sqr": 4, "mul": 5, "mul_add": 6, "mul_sub": 7,
+               "scale": 8, "Ax_plus_y": 9, "Ax_plus_By": 10, "from_std": 11, "to_std": 12, "copy": 13,
+               "set_const": 14, "inv": 15, "div": 16}
+
+
 # ----------------------------------------------------------------------------- synthetic inputs
 
 def gen_fr(curve, seed, count, start=0):
@@ -280,6 +464,15 @@ def msm_device(curve, n, d_scalars, d_points, mont=True, window=0):
     load().zkg_g1_msm_device(CURVE_ID[curve], n, d_scalars.ptr, 4, 1 if mont else 0, d_points.ptr, _p(out),
                              window)
     return out
+
+
+def arr_op_device(curve, op, n, d_a, d_b=None, d_c=None, kA=None, kB=None, d_tgt=None):
+    """device-resident Fr vector op (zkg_arr_op_device); d_* are DeviceBuffers"""
+    z = np.zeros(4, dtype=np.uint64)
+    ka = np.ascontiguousarray(kA if kA is not None else z, dtype=np.uint64)
+    kb = np.ascontiguousarray(kB if kB is not None else z, dtype=np.uint64)
+    load().zkg_arr_op_device(CURVE_ID[curve], ARR_OP_CODE[op], n, d_a.ptr if d_a else None,
+                             d_b.ptr if d_b else None, d_c.ptr if d_c else None, _p(ka), _p(kb), d_tgt.ptr)
 
 
 def ntt_device(curve, m, gen, d_src, d_dst, inverse=False):

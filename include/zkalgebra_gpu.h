@@ -78,6 +78,20 @@ ZKG_API void bn128_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint6
 ZKG_API void bls12_381_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
 ZKG_API void bls12_381_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
 
+/* G1 batch conversions and the group (curve) FFT.
+ *   bls12_381_G1_proj.h:9-10, 48-49 (bn128_G1_proj.h same lines); Haskell batchFromAffine /
+ *   batchToAffine (G1/Proj.hs:409-430), forwardFFT / inverseFFT = curveFFT / curveIFFT
+ *   (G1/Proj.hs:270-294).  Projective outputs of the FFT are normalised, like the
+ *   reference's (bls12_381_G1_proj.c:719, 785). */
+ZKG_API void bn128_G1_proj_batch_from_affine( int N, const uint64_t *src , uint64_t *tgt );
+ZKG_API void bn128_G1_proj_batch_to_affine  ( int N, const uint64_t *src , uint64_t *tgt );
+ZKG_API void bn128_G1_proj_fft_forward( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_G1_proj_fft_inverse( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_G1_proj_batch_from_affine( int N, const uint64_t *src , uint64_t *tgt );
+ZKG_API void bls12_381_G1_proj_batch_to_affine  ( int N, const uint64_t *src , uint64_t *tgt );
+ZKG_API void bls12_381_G1_proj_fft_forward( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_G1_proj_fft_inverse( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
+
 /* Fr vector operations around the NTT.  <C> in {bn128, bls12_381}.
  *   lib/cbits/curves/array/mont/bls12_381_arr_mont.h:3-48 (bn128_arr_mont.h same lines),
  *   bound by Haskell ZK.Algebra.Curves.<C>.Array (Array.hs:108-352).
@@ -198,6 +212,11 @@ ZKG_API void zkg_arr_powers_device(int curve, int n, const uint64_t *kA, const u
 ZKG_API int zkg_poly_div_by_vanishing_device(int curve, int n1, const uint64_t *d_src, int expo_n,
                                              const uint64_t *eta, int nquot, uint64_t *d_quot, int nrem,
                                              uint64_t *d_rem);
+
+/* device-resident G1 group FFT / batch_to_affine (d_* DEVICE pointers, gen on the host) */
+ZKG_API void zkg_g1_fft_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src,
+                               uint64_t *d_tgt);
+ZKG_API void zkg_g1_batch_to_affine_device(int curve, int n, const uint64_t *d_src, uint64_t *d_tgt);
 
 /* host helpers on G1 (projective, reference Montgomery form) */
 ZKG_API void zkg_g1_proj_add(int curve, const uint64_t *a, const uint64_t *b, uint64_t *out);

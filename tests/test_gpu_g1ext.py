@@ -1,0 +1,122 @@
+"""GPU G1 batch affine conversion and group FFT through the
+reference-named C ABI, bit-exact against the reference's own C (oracle/_ref):
+  <C>_G1_proj_batch_{from,to}_affine   bls12_381_G1_proj.c:147-167
+  <C>_G1_proj_fft_{forward,inverse}    bls12_381_G1_proj.c:679-790
+Inputs: projective points with non-trivial Z, points at infinity, and (BLS12-381) points
+OUTSIDE the order-r subgroup -- for those the result depends on the exact per-level
+scalars, so they pin the per-level structure, not just the linear map mod r."""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+CURVES = ["bn128", "bls12_381"]
+FP = {"bn128": 0, "bls12_381": 2}
+P_BLS = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+
+
+def to_limbs(x, n):
+    return np.array([(x >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(n)], dtype=np.uint64)
+
+
+def projective(gpu, oracle, curve, n, seed, n_inf=3):
+    """n projective points (X:Y:Z) = (x l : y l : l) with random l, a few at infinity"""
+    NP = gpu.NLIMBS_P[curve]
+    aff = gpu.gen_points(curve, seed, n)
+    lam = gpu.gen_points(curve, seed + 1, n)[:, :NP]  # random field elements (canonical)
+    out = np.zeros((n, 3 * NP), dtype=np.uint64)
+    for i in range(n):
+        for k in range(2):
+            oracle.lib.zko_fmul(FP[curve], _p(aff[i, k * NP:(k + 1) * NP]), _p(lam[i]),
+                                _p(out[i, k * NP:(k + 1) * NP]))
+        out[i, 2 * NP:] = lam[i]
+    rng = random.Random(seed)
+    for i in rng.sample(range(n), min(n_inf, n)):
+        out[i] = 0
+        out[i, NP:2 * NP] = lam[i]  # (0 : y : 0) with arbitrary y is infinity too
+    return out
+
+
+def _p(a):
+    import ctypes
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+def bls_nonsubgroup_points(n, seed):
+    """random points of E(Fp): y^2 = x^3 + 4, almost surely outside the order-r subgroup
+    (cofactor h ~ 2^126); Montgomery form (R = 2^384)"""
+    rng = random.Random(seed)
+    R = 1 << 384
+    pts = []
+    while len(pts) < n:
+        x = rng.randrange(P_BLS)
+        rhs = (x * x * x + 4) % P_BLS
+        y = pow(rhs, (P_BLS + 1) // 4, P_BLS)
+        if y * y % P_BLS != rhs:
+            continue
+        pts.append(np.concatenate([to_limbs(x * R % P_BLS, 6), to_limbs(y * R % P_BLS, 6)]))
+    return np.stack(pts)
+
+
+def ref_call(reference, curve, name, *args):
+    return reference.arr(curve, name, *args)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_batch_from_affine(gpu, reference, curve):
+    n = 1000
+    aff = gpu.gen_points(curve, 101, n)
+    aff[[3, 500]] = np.uint64(0xFFFFFFFFFFFFFFFF)  # affine infinity sentinel
+    want = np.zeros((n, 3 * gpu.NLIMBS_P[curve]), dtype=np.uint64)
+    ref_call(reference, curve, "G1_proj_batch_from_affine", n, aff, want)
+    assert np.array_equal(gpu.batch_from_affine(curve, aff), want)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("n", [1, 31, 33, 1000, 1 << 16])
+def test_batch_to_affine(gpu, oracle, reference, curve, n):
+    proj = projective(gpu, oracle, curve, n, 102 + n) if n <= 1000 else None
+    if proj is None:  # large: cheap inputs (Z = 1 after from_affine, plus infinities)
+        aff = gpu.gen_points(curve, 103, n)
+        aff[::1000] = np.uint64(0xFFFFFFFFFFFFFFFF)
+        proj = gpu.batch_from_affine(curve, aff)
+    want = np.zeros((n, 2 * gpu.NLIMBS_P[curve]), dtype=np.uint64)
+    ref_call(reference, curve, "G1_proj_batch_to_affine", n, proj, want)
+    assert np.array_equal(gpu.batch_to_affine(curve, proj), want)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("m", [0, 1, 2, 3, 5, 8])
+def test_fft_vs_reference(gpu, oracle, reference, curve, m):
+    n = 1 << m
+    pts = projective(gpu, oracle, curve, n, 200 + m, n_inf=min(2, n))
+    sg = gpu.get_fft_subgroup(curve, m)
+    for name, f in (("G1_proj_fft_forward", gpu.forward_fft), ("G1_proj_fft_inverse", gpu.inverse_fft)):
+        want = np.zeros_like(pts)
+        ref_call(reference, curve, name, m, sg.gen_array(), pts, want)
+        assert np.array_equal(f(sg, pts), want), (name, m)
+
+
+@pytest.mark.parametrize("m", [1, 3, 6])
+def test_fft_nonsubgroup_points_bls(gpu, reference, m):
+    """points outside the r-subgroup: only the exact per-level scalar schedule matches"""
+    curve = "bls12_381"
+    n = 1 << m
+    proj = gpu.batch_from_affine(curve, bls_nonsubgroup_points(n, 300 + m))
+    sg = gpu.get_fft_subgroup(curve, m)
+    for name, f in (("G1_proj_fft_forward", gpu.forward_fft), ("G1_proj_fft_inverse", gpu.inverse_fft)):
+        want = np.zeros_like(proj)
+        ref_call(reference, curve, name, m, sg.gen_array(), proj, want)
+        assert np.array_equal(f(sg, proj), want), (name, m)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_fft_roundtrip_2_12(gpu, curve):
+    """size-independent property at a larger size: iFFT(FFT(P)) = P for subgroup points"""
+    m = 12
+    aff = gpu.gen_points(curve, 400, 1 << m)
+    proj = gpu.batch_from_affine(curve, aff)
+    sg = gpu.get_fft_subgroup(curve, m)
+    back = gpu.inverse_fft(sg, gpu.forward_fft(sg, proj))
+    assert np.array_equal(back, proj)

@@ -1,5 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_arr.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t5.log 2>&1; rc=$?
-tail -30 gpurun_out/t5.log
+timeout -k 10 500 python -u -m pytest tests/test_gpu_g1ext.py -x -v --timeout 300 --timeout-method thread > gpurun_out/t6.log 2>&1; rc=$?
+grep -E "PASS|FAIL|Error|error" gpurun_out/t6.log | tail -40
 exit $rc

@@ -111,3 +111,35 @@ ZKG_API int zkg_poly_div_by_vanishing_device(int curve, int n1, const uint64_t *
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------- G1
+#include "zk_g1ext.hpp"
+
+extern "C" {
+
+#define ZKG_G1EXT_ENTRIES(PFX, CID)                                                                         \
+  ZKG_API void PFX##_G1_proj_batch_from_affine(int N, const uint64_t *src, uint64_t *tgt) {                 \
+    g1_batch_from_affine(CID, N, src, tgt, true);                                                           \
+  }                                                                                                         \
+  ZKG_API void PFX##_G1_proj_batch_to_affine(int N, const uint64_t *src, uint64_t *tgt) {                   \
+    g1_batch_to_affine(CID, N, src, tgt, true);                                                             \
+  }                                                                                                         \
+  ZKG_API void PFX##_G1_proj_fft_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {  \
+    g1_fft(CID, m, gen, src, tgt, true, false);                                                             \
+  }                                                                                                         \
+  ZKG_API void PFX##_G1_proj_fft_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {  \
+    g1_fft(CID, m, gen, src, tgt, true, true);                                                              \
+  }
+
+ZKG_G1EXT_ENTRIES(bn128, ZKG_BN128)
+ZKG_G1EXT_ENTRIES(bls12_381, ZKG_BLS12_381)
+
+ZKG_API void zkg_g1_fft_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src,
+                               uint64_t *d_tgt) {
+  g1_fft(curve, m, gen, d_src, d_tgt, false, inverse != 0);
+}
+ZKG_API void zkg_g1_batch_to_affine_device(int curve, int n, const uint64_t *d_src, uint64_t *d_tgt) {
+  g1_batch_to_affine(curve, n, d_src, d_tgt, false);
+}
+
+}  // extern "C"

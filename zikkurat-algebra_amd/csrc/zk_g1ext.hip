@@ -1,0 +1,511 @@
+// zk_g1ext.hip -- G1 batch affine conversion and the group (curve) FFT on gfx950.
+//
+// Replaces:
+//   <C>_G1_proj_batch_from_affine / _batch_to_affine  bls12_381_G1_proj.c:147-167
+//        (Haskell batchFromAffine / batchToAffine, G1/Proj.hs:409-430; msmProj, :222-223)
+//   <C>_G1_proj_fft_forward / _fft_inverse            bls12_381_G1_proj.c:679-790
+//        (Haskell forwardFFT / inverseFFT = curveFFT / curveIFFT, G1/Proj.hs:270-294)
+//
+// batch_to_affine: the reference inverts every Z separately (Fp_mont_inv per point,
+// G1_proj.c:133-145); here CHK consecutive points per lane share ONE Fermat inversion
+// (Montgomery's trick), points at infinity (Z = 0) are skipped in the product and come
+// out as the all-0xFF affine sentinel, exactly like the reference.
+//
+// Group FFT: the reference recursion (radix-2 DIT forward; DIF with a factor 1/2 per
+// level inverse) multiplies points by canonical Fr scalars at every level:
+//   forward level s: t = w_s^j * v,  (u + t, u - t)
+//   inverse level s: ((u + v) * 1/2,  (u - v) * (w_s^-j / 2))
+// Scalar multiplication is by the INTEGER value of the canonical scalar, so for points
+// outside the order-r subgroup (BLS12-381 G1 has a cofactor) the result depends on the
+// exact per-level scalars, not only on their product mod r.  This implementation applies
+// the same per-level scalars at the same positions (iterative DIT / DIF over HBM,
+// ping-pong buffers), so its output is bit-identical for every on-curve input.
+// Scalar multiplication: fixed 4-bit windows, MSB first, 15-entry table per lane in
+// global scratch (no lane divergence on the digit: every window does one table add).
+// Outputs are normalised (Z = 1, infinity = (0:1:0)) as the reference does (:719, :785).
+#include "zk_curve.hpp"
+#include "zk_host.hpp"
+#include "zk_msm.hpp"
+#include "zk_runtime.hpp"
+#include "zk_g1ext.hpp"
+
+namespace zk {
+
+struct W6 {
+  uint64_t w[6];
+};
+
+template <class F>
+__device__ __forceinline__ void xyzz_store(uint32_t *p, const Xyzz<F> &a) {
+  fe_store_u(p + 0 * F::SN, a.X);
+  fe_store_u(p + 1 * F::SN, a.Y);
+  fe_store_u(p + 2 * F::SN, a.ZZ);
+  fe_store_u(p + 3 * F::SN, a.ZZZ);
+}
+template <class F>
+__device__ __forceinline__ void xyzz_load(Xyzz<F> &a, const uint32_t *p) {
+  fe_load_u(a.X, p + 0 * F::SN);
+  fe_load_u(a.Y, p + 1 * F::SN);
+  fe_load_u(a.ZZ, p + 2 * F::SN);
+  fe_load_u(a.ZZZ, p + 3 * F::SN);
+}
+template <class F>
+constexpr int xw() { return 4 * F::SN; }  // u32 words per stored XYZZ point
+
+// x^e for an NW-word exponent, square-and-multiply MSB first (uniform across lanes)
+template <class F, int NW>
+__device__ __forceinline__ void fe_pow_words(Fe<F> &r, const Fe<F> &x, const W6 &e) {
+  Fe<F> acc, t;
+  fe_one(acc);
+  for (int w = NW - 1; w >= 0; w--) {
+    const uint64_t ew = e.w[w];
+    for (int b = 63; b >= 0; b--) {
+      fe_sqr(t, acc);
+      acc = t;
+      if ((ew >> b) & 1) {
+        fe_mul(t, acc, x);
+        acc = t;
+      }
+    }
+  }
+  r = acc;
+}
+
+template <class F>
+__device__ __forceinline__ void ld_int(Fe<F> &r, const uint64_t *p) {  // reference form -> internal
+  Fe<F> t;
+  fe_load_ref(t, p);
+  fe_to_int(r, t);
+}
+template <class F>
+__device__ __forceinline__ void st_ref(uint64_t *p, const Fe<F> &a) {  // internal -> canonical reference form
+  Fe<F> t;
+  fe_to_ref(t, a);
+  fe_store_ref(p, t);
+}
+template <class F>
+__device__ __forceinline__ bool ref_all_ones(const uint64_t *p, int words) {
+  uint64_t a = ~0ull;
+  for (int i = 0; i < words; i++) a &= p[i];
+  return a == ~0ull;
+}
+
+// ---------------------------------------------------------------------------- batch_from_affine
+
+template <class C>
+__global__ void __launch_bounds__(256) k_from_affine(int n, const uint64_t *__restrict__ src,
+                                                     uint64_t *__restrict__ tgt, W6 one_ref) {
+  constexpr int NP = C::NP64;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)n) return;
+  const uint64_t *a = src + i * 2 * NP;
+  uint64_t *o = tgt + i * 3 * NP;
+  if (ref_all_ones<typename C::Fp>(a, 2 * NP)) {  // affine infinity -> (0 : 1 : 0), G1_proj.c:121-129
+    for (int k = 0; k < NP; k++) { o[k] = 0; o[NP + k] = one_ref.w[k]; o[2 * NP + k] = 0; }
+  } else {
+    for (int k = 0; k < 2 * NP; k++) o[k] = a[k];
+    for (int k = 0; k < NP; k++) o[2 * NP + k] = one_ref.w[k];
+  }
+}
+
+// ---------------------------------------------------------------------------- chunked inversion
+// MODE_PROJ_TO_AFF : src = reference projective (X:Y:Z), tgt = affine (X/Z, Y/Z) / 0xFF..
+// MODE_XYZZ_TO_PROJ: src = device XYZZ, tgt = normalised reference projective, written at
+//                    index bitrev_m(i) when m >= 0 (inverse FFT output order)
+enum { MODE_PROJ_TO_AFF = 0, MODE_XYZZ_TO_PROJ = 1 };
+
+template <class C, int MODE>
+__global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void *__restrict__ srcv,
+                                                     uint64_t *__restrict__ scratch, uint64_t *__restrict__ tgt,
+                                                     W6 pm2, int bitrev_m) {
+  using F = typename C::Fp;
+  constexpr int NP = C::NP64;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i0 = t * CHK;
+  if (i0 >= (size_t)n) return;
+  const size_t i1 = min((size_t)n, i0 + CHK);
+  const uint64_t *srcp = reinterpret_cast<const uint64_t *>(srcv);
+  const uint32_t *srcx = reinterpret_cast<const uint32_t *>(srcv);
+  auto den = [&](size_t i, Fe<F> &d) -> bool {  // denominator (internal); false = infinity
+    if (MODE == MODE_PROJ_TO_AFF) {
+      ld_int(d, srcp + i * 3 * NP + 2 * NP);
+    } else {
+      fe_load_u(d, srcx + i * xw<F>() + 3 * F::SN);  // ZZZ
+    }
+    return !fe_is_zero(d);
+  };
+  Fe<F> P;
+  fe_one(P);
+  for (size_t i = i0; i < i1; i++) {
+    Fe<F> d, q;
+    if (den(i, d)) {
+      fe_mul(q, P, d);
+      P = q;
+    }
+    fe_store_ref(scratch + i * NP, P);  // running product (internal form, packed)
+  }
+  Fe<F> inv;
+  fe_pow_words<F, NP>(inv, P, pm2);
+  Fe<F> one_int;
+  fe_one(one_int);
+  for (size_t i = i1; i-- > i0;) {
+    Fe<F> d;
+    const bool fin = den(i, d);
+    size_t o = i;
+    if (MODE == MODE_XYZZ_TO_PROJ && bitrev_m > 0)
+      o = (size_t)(__builtin_bitreverse32((uint32_t)i) >> (32 - bitrev_m));
+    if (!fin) {
+      if (MODE == MODE_PROJ_TO_AFF) {
+        for (int k = 0; k < 2 * NP; k++) tgt[o * 2 * NP + k] = ~0ull;  // G1_proj.c:134-138
+      } else {
+        uint64_t *q = tgt + o * 3 * NP;
+        for (int k = 0; k < NP; k++) q[k] = 0;
+        st_ref(q + NP, one_int);
+        for (int k = 0; k < NP; k++) q[2 * NP + k] = 0;
+      }
+      continue;
+    }
+    Fe<F> prev, dinv, q;
+    if (i > i0) fe_load_ref(prev, scratch + (i - 1) * NP); else prev = one_int;
+    fe_mul(dinv, inv, prev);  // 1 / d_i
+    fe_mul(q, inv, d);
+    inv = q;
+    if (MODE == MODE_PROJ_TO_AFF) {
+      Fe<F> X, Y, x, y;
+      ld_int(X, srcp + i * 3 * NP);
+      ld_int(Y, srcp + i * 3 * NP + NP);
+      fe_mul(x, X, dinv);
+      fe_mul(y, Y, dinv);
+      st_ref(tgt + o * 2 * NP, x);
+      st_ref(tgt + o * 2 * NP + NP, y);
+    } else {
+      Xyzz<F> p;
+      xyzz_load(p, srcx + i * xw<F>());
+      Fe<F> iz, iz2, x, y;
+      fe_mul(iz, p.ZZ, dinv);  // ZZ / ZZZ = 1/Z
+      fe_sqr(iz2, iz);         // 1/ZZ
+      fe_mul(x, p.X, iz2);
+      fe_mul(y, p.Y, dinv);
+      uint64_t *qo = tgt + o * 3 * NP;
+      st_ref(qo, x);
+      st_ref(qo + NP, y);
+      st_ref(qo + 2 * NP, one_int);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- group FFT
+
+// reference projective -> device XYZZ (x = X/Z -> X' = X Z, ZZ = Z^2; y = Y/Z -> Y' = Y Z^2,
+// ZZZ = Z^3), stored at bitrev_m(i) when m > 0 (forward FFT input order)
+template <class C>
+__global__ void __launch_bounds__(256) k_fft_load(int n, int bitrev_m, const uint64_t *__restrict__ src,
+                                                  uint32_t *__restrict__ dst) {
+  using F = typename C::Fp;
+  constexpr int NP = C::NP64;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)n) return;
+  Fe<F> X, Y, Z;
+  ld_int(X, src + i * 3 * NP);
+  ld_int(Y, src + i * 3 * NP + NP);
+  ld_int(Z, src + i * 3 * NP + 2 * NP);
+  Xyzz<F> p;
+  if (fe_is_zero(Z)) {
+    xyzz_set_inf(p);
+  } else {
+    fe_sqr(p.ZZ, Z);
+    fe_mul(p.ZZZ, p.ZZ, Z);
+    fe_mul(p.X, X, Z);
+    fe_mul(p.Y, Y, p.ZZ);
+  }
+  const size_t o = bitrev_m > 0 ? (size_t)(__builtin_bitreverse32((uint32_t)i) >> (32 - bitrev_m)) : i;
+  xyzz_store(dst + o * xw<F>(), p);
+}
+
+template <class F>
+__device__ __forceinline__ void xyzz_neg(Xyzz<F> &r, const Xyzz<F> &a) {
+  r = a;
+  fe_neg(r.Y, a.Y);
+}
+
+// r = k * P, k a 256-bit integer (4 u64), fixed 4-bit windows MSB first; tab = this lane's
+// 15-point scratch table (tab[d-1] = d P)
+template <class F>
+__device__ void xyzz_scl(Xyzz<F> &r, const Xyzz<F> &P, const uint64_t *k, uint32_t *__restrict__ tab) {
+  {
+    Xyzz<F> acc = P;
+    xyzz_store(tab, acc);
+    for (int d = 2; d <= 15; d++) {
+      if (d == 2) xyzz_dbl(acc, P);
+      else xyzz_add(acc, P);
+      xyzz_store(tab + (size_t)(d - 1) * xw<F>(), acc);
+    }
+  }
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  for (int w = 63; w >= 0; w--) {
+    if (w != 63) {
+      for (int q = 0; q < 4; q++) {
+        Xyzz<F> t;
+        xyzz_dbl(t, acc);
+        acc = t;
+      }
+    }
+    const uint32_t d = (uint32_t)(k[w >> 4] >> ((w & 15) * 4)) & 15u;
+    if (d) {
+      Xyzz<F> e;
+      xyzz_load(e, tab + (size_t)(d - 1) * xw<F>());
+      xyzz_add(acc, e);
+    }
+  }
+  r = acc;
+}
+
+// forward DIT stage s (block 2^s): lane = butterfly (blk, j); t = w_s^j v (w_s^j = tw[j 2^(m-s)],
+// canonical Fr in standard form, = 1 for j = 0); out = (u + t, u - t)
+template <class C>
+__global__ void __launch_bounds__(256) k_fft_fwd_stage(int m, int s, const uint32_t *__restrict__ A,
+                                                       uint32_t *__restrict__ B, const uint64_t *__restrict__ tw,
+                                                       uint32_t *__restrict__ scratch, int lanes) {
+  using F = typename C::Fp;
+  const int half = 1 << (s - 1);
+  const size_t nb = (size_t)1 << (m - 1);
+  for (size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (size_t)lanes) {
+    const size_t blk = b >> (s - 1), j = b & (half - 1);
+    const size_t k0 = (blk << s) + j;
+    Xyzz<F> u, v, t;
+    xyzz_load(u, A + k0 * xw<F>());
+    xyzz_load(v, A + (k0 + half) * xw<F>());
+    if (j == 0) {
+      t = v;
+    } else {
+      const uint64_t *k = tw + (j << (m - s)) * 4;
+      xyzz_scl(t, v, k, scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 15 * xw<F>());
+    }
+    Xyzz<F> x = u, nt;
+    xyzz_add(x, t);
+    xyzz_neg(nt, t);
+    xyzz_add(u, nt);
+    xyzz_store(B + k0 * xw<F>(), x);
+    xyzz_store(B + (k0 + half) * xw<F>(), u);
+  }
+}
+
+// inverse DIF stage s: lane = output (butterfly, which): which 0 -> (u + v) * 1/2,
+// which 1 -> (u - v) * (w_s^-j / 2) (tw[e] = inv(w)^e / 2, standard form); half = std(1/2)
+template <class C>
+__global__ void __launch_bounds__(256) k_fft_inv_stage(int m, int s, const uint32_t *__restrict__ A,
+                                                       uint32_t *__restrict__ B, const uint64_t *__restrict__ tw,
+                                                       uint32_t *__restrict__ scratch, int lanes) {
+  using F = typename C::Fp;
+  const int half = 1 << (s - 1);
+  const size_t no = (size_t)1 << m;
+  for (size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x; o < no; o += (size_t)lanes) {
+    const size_t b = o >> 1;
+    const int which = (int)(o & 1);
+    const size_t blk = b >> (s - 1), j = b & (half - 1);
+    const size_t k0 = (blk << s) + j;
+    Xyzz<F> u, v, t;
+    xyzz_load(u, A + k0 * xw<F>());
+    xyzz_load(v, A + (k0 + half) * xw<F>());
+    if (which == 0) {
+      xyzz_add(u, v);
+    } else {
+      Xyzz<F> nv;
+      xyzz_neg(nv, v);
+      xyzz_add(u, nv);
+    }
+    const uint64_t *k = tw + (which ? (j << (m - s)) : 0) * 4;  // tw[0] = 1/2
+    xyzz_scl(t, u, k, scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 15 * xw<F>());
+    xyzz_store(B + (k0 + (which ? half : 0)) * xw<F>(), t);
+  }
+}
+
+// tw[e] = std(scale * base^e) for e < cnt (base, scale: Fr reference Montgomery form)
+template <class Fr>
+__global__ void __launch_bounds__(256) k_fft_tw(int cnt, W6 base, W6 scale, uint64_t *__restrict__ tw) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= cnt) return;
+  Fe<Fr> b, acc, t;
+  ld_int(b, base.w);
+  fe_load_ref(acc, scale.w);  // reference form
+  Fe<Fr> p = b;
+  for (int x = e; x; x >>= 1) {
+    if (x & 1) { fe_mul(t, acc, p); acc = t; }
+    fe_sqr(t, p);
+    p = t;
+  }
+  Fe<Fr> sd;
+  fe_ref_to_std(sd, acc);
+  fe_store_ref(tw + (size_t)e * 4, sd);
+}
+
+// ---------------------------------------------------------------------------- host side
+
+template <class HF>
+static W6 exp_p_minus_2() {
+  W6 e = {{0, 0, 0, 0, 0, 0}};
+  for (int j = 0; j < HF::N; j++) e.w[j] = HF::P[j];
+  uint64_t br = 2;
+  for (int j = 0; j < HF::N && br; j++) {
+    const uint64_t o = e.w[j];
+    e.w[j] = o - br;
+    br = o < br ? 1 : 0;
+  }
+  return e;
+}
+template <class HF>
+static W6 one_ref() {
+  W6 o = {{0, 0, 0, 0, 0, 0}};
+  for (int j = 0; j < HF::N; j++) o.w[j] = HF::ONE[j];
+  return o;
+}
+
+template <class C>
+static void batch_from_affine_t(Device &dev, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
+  using HF = typename HostOf<C>::Fp;
+  constexpr int NP = C::NP64;
+  if (n <= 0) return;
+  hipStream_t st = dev.stream;
+  const size_t N = (size_t)n;
+  dev.arena.reserve(N * 5 * NP * 8 + (1 << 20));
+  dev.arena.reset();
+  const uint64_t *ds = src;
+  uint64_t *dt = tgt;
+  if (host_io) {
+    uint64_t *a = dev.arena.take<uint64_t>(N * 2 * NP);
+    ZK_CHECK(hipMemcpyAsync(a, src, N * 2 * NP * 8, hipMemcpyHostToDevice, st));
+    ds = a;
+    dt = dev.arena.take<uint64_t>(N * 3 * NP);
+  }
+  hipLaunchKernelGGL(k_from_affine<C>, dim3(div_up(N, 256)), dim3(256), 0, st, n, ds, dt, one_ref<HF>());
+  ZK_CHECK(hipGetLastError());
+  if (host_io) ZK_CHECK(hipMemcpyAsync(tgt, dt, N * 3 * NP * 8, hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+}
+
+static const int NORM_CHK = 32;
+
+template <class C>
+static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
+  using HF = typename HostOf<C>::Fp;
+  constexpr int NP = C::NP64;
+  if (n <= 0) return;
+  hipStream_t st = dev.stream;
+  const size_t N = (size_t)n;
+  dev.arena.reserve(N * 6 * NP * 8 + (1 << 20));
+  dev.arena.reset();
+  const uint64_t *ds = src;
+  uint64_t *dt = tgt;
+  if (host_io) {
+    uint64_t *a = dev.arena.take<uint64_t>(N * 3 * NP);
+    ZK_CHECK(hipMemcpyAsync(a, src, N * 3 * NP * 8, hipMemcpyHostToDevice, st));
+    ds = a;
+    dt = dev.arena.take<uint64_t>(N * 2 * NP);
+  }
+  uint64_t *scratch = dev.arena.take<uint64_t>(N * NP);
+  const size_t lanes = (N + NORM_CHK - 1) / NORM_CHK;
+  hipLaunchKernelGGL((k_norm_chunks<C, MODE_PROJ_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, NORM_CHK,
+                     (const void *)ds, scratch, dt, exp_p_minus_2<HF>(), 0);
+  ZK_CHECK(hipGetLastError());
+  if (host_io) ZK_CHECK(hipMemcpyAsync(tgt, dt, N * 2 * NP * 8, hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+}
+
+template <class C>
+static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io,
+                     bool inverse) {
+  using F = typename C::Fp;
+  using HF = typename HostOf<C>::Fp;
+  using HR = typename HostOf<C>::Fr;
+  using Fr = typename C::Fr;
+  constexpr int NP = C::NP64;
+  ZK_REQUIRE(m >= 0 && m <= 26, "G1 fft: log2 size out of range (0..26)");
+  hipStream_t st = dev.stream;
+  const size_t N = (size_t)1 << m;
+  // scalar-multiplication lanes are grid-strided so the per-lane table scratch stays bounded
+  const size_t work = inverse ? N : N / 2;
+  size_t lanes = work < (1u << 17) ? work : (1u << 17);
+  lanes = (lanes + 255) & ~(size_t)255;
+  if (lanes == 0) lanes = 256;
+  const size_t tw_cnt = N > 1 ? N / 2 : 1;
+  dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 2 * N * xw<F>() * 4 + lanes * 15 * xw<F>() * 4 +
+                    tw_cnt * 32 + N * NP * 8 + (1 << 20));
+  dev.arena.reset();
+  const uint64_t *ds = src;
+  uint64_t *dt = tgt;
+  if (host_io) {
+    uint64_t *a = dev.arena.take<uint64_t>(N * 3 * NP);
+    ZK_CHECK(hipMemcpyAsync(a, src, N * 3 * NP * 8, hipMemcpyHostToDevice, st));
+    ds = a;
+    dt = dev.arena.take<uint64_t>(N * 3 * NP);
+  }
+  uint32_t *A = dev.arena.take<uint32_t>(N * xw<F>());
+  uint32_t *B = dev.arena.take<uint32_t>(N * xw<F>());
+  uint32_t *scratch = dev.arena.take<uint32_t>(lanes * 15 * xw<F>());
+  uint64_t *tw = dev.arena.take<uint64_t>(tw_cnt * 4);
+  uint64_t *nscratch = dev.arena.take<uint64_t>(N * NP);
+
+  hipLaunchKernelGGL(k_fft_load<C>, dim3(div_up(N, 256)), dim3(256), 0, st, (int)N, inverse ? 0 : m, ds, A);
+  ZK_CHECK(hipGetLastError());
+  if (m > 0) {
+    // twiddles: forward w^e; inverse (w^-1)^e / 2 -- the reference's gpow sequences
+    // (G1_proj.c:705-711, 758-764), canonical Fr, standard form
+    zkh::Fe<HR> g, scale;
+    memcpy(g.v, gen, sizeof g.v);
+    zkh::set_one(scale);
+    if (inverse) {
+      zkh::inv(g, g);
+      zkh::Fe<HR> two;
+      zkh::add(two, scale, scale);
+      zkh::inv(scale, two);  // Montgomery(1/2) = the reference's oneHalf (G1_proj.c:727)
+    }
+    W6 wb = {{0, 0, 0, 0, 0, 0}}, ws = {{0, 0, 0, 0, 0, 0}};
+    for (int j = 0; j < 4; j++) { wb.w[j] = g.v[j]; ws.w[j] = scale.v[j]; }
+    hipLaunchKernelGGL(k_fft_tw<Fr>, dim3(div_up(tw_cnt, 256)), dim3(256), 0, st, (int)tw_cnt, wb, ws, tw);
+    ZK_CHECK(hipGetLastError());
+    const unsigned grid = (unsigned)(lanes / 256);
+    uint32_t *in = A, *out = B;
+    for (int k = 0; k < m; k++) {
+      const int s = inverse ? m - k : k + 1;
+      if (inverse)
+        hipLaunchKernelGGL(k_fft_inv_stage<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, tw, scratch, (int)lanes);
+      else
+        hipLaunchKernelGGL(k_fft_fwd_stage<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, tw, scratch, (int)lanes);
+      ZK_CHECK(hipGetLastError());
+      uint32_t *x = in;
+      in = out;
+      out = x;
+    }
+    A = in;
+  }
+  const size_t nl = (N + NORM_CHK - 1) / NORM_CHK;
+  hipLaunchKernelGGL((k_norm_chunks<C, MODE_XYZZ_TO_PROJ>), dim3(div_up(nl, 256)), dim3(256), 0, st, (int)N,
+                     NORM_CHK, (const void *)A, nscratch, dt, exp_p_minus_2<HF>(), inverse ? m : 0);
+  ZK_CHECK(hipGetLastError());
+  if (host_io) ZK_CHECK(hipMemcpyAsync(tgt, dt, N * 3 * NP * 8, hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+}
+
+// ---------------------------------------------------------------------------- public
+
+void g1_batch_from_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  if (curve == 0) batch_from_affine_t<BN254>(dev, n, src, tgt, host_io);
+  else batch_from_affine_t<BLS381>(dev, n, src, tgt, host_io);
+}
+void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  if (curve == 0) batch_to_affine_t<BN254>(dev, n, src, tgt, host_io);
+  else batch_to_affine_t<BLS381>(dev, n, src, tgt, host_io);
+}
+void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse) {
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  if (curve == 0) g1_fft_t<BN254>(dev, m, gen, src, tgt, host_io, inverse);
+  else g1_fft_t<BLS381>(dev, m, gen, src, tgt, host_io, inverse);
+}
+
+}  // namespace zk

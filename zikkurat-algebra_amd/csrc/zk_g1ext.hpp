@@ -1,0 +1,14 @@
+// zk_g1ext.hpp -- C++ interface of the G1 batch conversions and the group FFT (zk_g1ext.hip)
+#pragma once
+#include <stdint.h>
+
+namespace zk {
+
+// affine (x || y, all-0xFF = infinity) -> projective (x : y : 1), infinity -> (0 : 1 : 0)
+void g1_batch_from_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io);
+// projective -> affine (X/Z, Y/Z), Z = 0 -> all-0xFF
+void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io);
+// group FFT of 2^m projective points with Fr generator `gen` (host, Montgomery); outputs normalised
+void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse);
+
+}  // namespace zk

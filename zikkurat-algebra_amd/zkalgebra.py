@@ -48,14 +48,16 @@ ARR_OPS = ["is_valid", "is_zero", "is_one", "is_equal", "set_zero", "set_one", "
            "mul_add", "mul_sub", "dot_prod", "powers", "scale", "scale_inplace", "Ax_plus_y", "Ax_plus_y_inplace",
            "Ax_plus_By", "Ax_plus_By_inplace"]
 REFERENCE_SYMBOLS += [f"{c}_arr_mont_{o}" for c in CURVES for o in ARR_OPS] + [
-    f"{c}_poly_mont_{k}_by_vanishing" for c in CURVES for k in ("div", "quot")]
+    f"{c}_poly_mont_{k}_by_vanishing" for c in CURVES for k in ("div", "quot")] + [
+    f"{c}_G1_proj_{f}" for c in CURVES for f in ("batch_from_affine", "batch_to_affine", "fft_forward",
+                                                  "fft_inverse")]
 EXTENSION_SYMBOLS = [
     "zkg_version", "zkg_device_count", "zkg_set_device", "zkg_device_malloc", "zkg_device_free",
     "zkg_memcpy_htod", "zkg_memcpy_dtoh", "zkg_device_synchronize", "zkg_g1_msm_device", "zkg_ntt_device",
     "zkg_g1_proj_add", "zkg_g1_proj_normalize", "zkg_g1_proj_to_affine", "zkg_gen_fr", "zkg_gen_g1_points",
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
     "zkg_field_mul_rate", "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
-    "zkg_poly_div_by_vanishing_device",
+    "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device",
 ]
 
 _lib = None
@@ -221,6 +223,48 @@ def g1_add(curve, a, b):
     out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
     load().zkg_g1_proj_add(CURVE_ID[curve], _p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(b)), _p(out))
     return out
+
+
+def batch_from_affine(curve, aff):
+    """Proj.batchFromAffine (G1/Proj.hs:409-418)"""
+    aff = np.ascontiguousarray(aff, dtype=np.uint64)
+    out = np.zeros((aff.shape[0], 3 * NLIMBS_P[curve]), dtype=np.uint64)
+    require_gpu()
+    getattr(load(), f"{curve}_G1_proj_batch_from_affine")(aff.shape[0], _p(aff), _p(out))
+    return out
+
+
+def batch_to_affine(curve, proj):
+    """Proj.batchToAffine (G1/Proj.hs:420-430); infinity -> all-0xFF"""
+    proj = np.ascontiguousarray(proj, dtype=np.uint64)
+    out = np.zeros((proj.shape[0], 2 * NLIMBS_P[curve]), dtype=np.uint64)
+    require_gpu()
+    getattr(load(), f"{curve}_G1_proj_batch_to_affine")(proj.shape[0], _p(proj), _p(out))
+    return out
+
+
+def _curve_fft(sg, pts, name, msg):
+    pts = np.ascontiguousarray(pts, dtype=np.uint64)
+    if pts.ndim != 2 or sg.size != pts.shape[0]:
+        raise ValueError(msg)
+    require_gpu()
+    out = np.zeros_like(pts)
+    getattr(load(), f"{sg.curve}_G1_proj_{name}")(sg.log_size, _p(sg.gen_array()), _p(pts), _p(out))
+    return out
+
+
+def forward_fft(sg, pts):
+    """Proj.forwardFFT = curveFFT (G1/Proj.hs:270-281): [L_k(tau)] -> [tau^i] points, normalised"""
+    return _curve_fft(sg, pts, "fft_forward", "forwardNTT: subgroup size differs from the array size")
+
+
+def inverse_fft(sg, pts):
+    """Proj.inverseFFT = curveIFFT (G1/Proj.hs:283-294): [tau^i] -> [L_k(tau)] points, normalised"""
+    return _curve_fft(sg, pts, "fft_inverse", "inverseNTT: subgroup size differs from the array size")
+
+
+curve_fft = forward_fft
+curve_ifft = inverse_fft
 
 
 # ----------------------------------------------------------------------------- NTT

@@ -78,6 +78,18 @@ ZKG_API void bn128_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint6
 ZKG_API void bls12_381_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
 ZKG_API void bls12_381_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt);
 
+/* MSM on G2: the twist over Fp2 = Fp[u]/(u^2+1), same conventions
+ * as G1 with NP doubled (Fp2 element = c0 || c1); affine infinity = all-0xFF.
+ *   bls12_381_G2_proj.h:43-46 (bn128_G2_proj.h same lines), bound by G2/Proj.hs */
+ZKG_API void bn128_G2_proj_MSM_std_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G2_proj_MSM_mont_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G2_proj_MSM_std_coeff_affine_out (int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bn128_G2_proj_MSM_mont_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G2_proj_MSM_std_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G2_proj_MSM_mont_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G2_proj_MSM_std_coeff_affine_out (int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+ZKG_API void bls12_381_G2_proj_MSM_mont_coeff_affine_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
+
 /* G1 batch conversions and the group (curve) FFT.
  *   bls12_381_G1_proj.h:9-10, 48-49 (bn128_G1_proj.h same lines); Haskell batchFromAffine /
  *   batchToAffine (G1/Proj.hs:409-430), forwardFFT / inverseFFT = curveFFT / curveIFFT
@@ -197,6 +209,9 @@ ZKG_API void zkg_device_synchronize(void);
 /* device-resident MSM: d_expos / d_grps are DEVICE pointers (already in HBM);
  * tgt_proj is a HOST buffer of 3*NP u64 receiving the normalised projective sum. */
 ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,
+                               const uint64_t *d_grps, uint64_t *tgt_proj, int window_size);
+/* device-resident G2 MSM (same contract as zkg_g1_msm_device; tgt_proj = 3 Fp2 elements) */
+ZKG_API void zkg_g2_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,
                                const uint64_t *d_grps, uint64_t *tgt_proj, int window_size);
 /* device-resident NTT: d_src / d_tgt DEVICE pointers; gen on the host */
 ZKG_API void zkg_ntt_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src, uint64_t *d_tgt);

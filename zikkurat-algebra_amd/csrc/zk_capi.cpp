@@ -97,6 +97,28 @@ extern "C" {
 ZKG_MSM_ENTRIES(bn128, BN254)
 ZKG_MSM_ENTRIES(bls12_381, BLS381)
 
+// G2 MSM: <C>_G2_proj_MSM_* (bls12_381_G2_proj.h:43-46)
+#define ZKG_G2_MSM_ENTRIES(PFX, CURVE)                                                                          \
+  ZKG_API void PFX##_G2_proj_MSM_mont_coeff_proj_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,  \
+                                                     int nl) {                                                  \
+    msm_entry<CURVE>(n, e, g, t, nl, true, 0, PROJ);                                                           \
+  }                                                                                                             \
+  ZKG_API void PFX##_G2_proj_MSM_std_coeff_proj_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,   \
+                                                    int nl) {                                                   \
+    msm_entry<CURVE>(n, e, g, t, nl, false, 0, PROJ);                                                          \
+  }                                                                                                             \
+  ZKG_API void PFX##_G2_proj_MSM_mont_coeff_affine_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t, \
+                                                       int nl) {                                                \
+    msm_entry<CURVE>(n, e, g, t, nl, true, 0, AFFINE);                                                         \
+  }                                                                                                             \
+  ZKG_API void PFX##_G2_proj_MSM_std_coeff_affine_out(int n, const uint64_t *e, const uint64_t *g, uint64_t *t,  \
+                                                      int nl) {                                                 \
+    msm_entry<CURVE>(n, e, g, t, nl, false, 0, AFFINE);                                                        \
+  }
+
+ZKG_G2_MSM_ENTRIES(bn128, BN254_G2)
+ZKG_G2_MSM_ENTRIES(bls12_381, BLS381_G2)
+
 ZKG_API void bn128_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
   zk::ntt(ZKG_BN128, m, gen, src, tgt, true, false);
 }
@@ -147,6 +169,26 @@ ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, 
     uint64_t p[18];
     msm_g1<BLS381>(npoints, d_expos, expo_nlimbs, d_grps, false, expos_mont != 0, c, p);
     zkg_g1_proj_normalize(curve, p, tgt_proj);
+  }
+}
+
+ZKG_API void zkg_g2_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,
+                               const uint64_t *d_grps, uint64_t *tgt_proj, int window_size) {
+  int c = window_size <= 0 ? 0 : (window_size < 4 ? 4 : (window_size > 24 ? 24 : window_size));
+  if (curve == ZKG_BN128) {
+    uint64_t p[24];
+    msm_g1<BN254_G2>(npoints, d_expos, expo_nlimbs, d_grps, false, expos_mont != 0, c, p);
+    zkh::Proj<HostOf<BN254_G2>::Fp> q, r;
+    memcpy(&q, p, sizeof q);
+    zkh::proj_normalize(r, q);
+    memcpy(tgt_proj, &r, sizeof r);
+  } else {
+    uint64_t p[36];
+    msm_g1<BLS381_G2>(npoints, d_expos, expo_nlimbs, d_grps, false, expos_mont != 0, c, p);
+    zkh::Proj<HostOf<BLS381_G2>::Fp> q, r;
+    memcpy(&q, p, sizeof q);
+    zkh::proj_normalize(r, q);
+    memcpy(tgt_proj, &r, sizeof r);
   }
 }
 

@@ -12,6 +12,7 @@
 // infinity as all-0xFF bytes (bls12_381_G1_affine.c:1-6, :63-66).
 #pragma once
 #include "zk_field.hpp"
+#include "zk_field2.hpp"
 
 namespace zk {
 
@@ -25,6 +26,17 @@ struct BLS381 {
   using Fp = BLS_Fp;
   using Fr = BLS_Fr;
   static constexpr int NP64 = ZK_BLS12_381_FP_N64;
+};
+// G2: the twists over Fp2 (a = 0 as well; the XYZZ formulas never use b)
+struct BN254_G2 {
+  using Fp = F2<BN_Fp>;
+  using Fr = BN_Fr;
+  static constexpr int NP64 = 2 * ZK_BN128_FP_N64;
+};
+struct BLS381_G2 {
+  using Fp = F2<BLS_Fp>;
+  using Fr = BLS_Fr;
+  static constexpr int NP64 = 2 * ZK_BLS12_381_FP_N64;
 };
 
 template <class F>
@@ -241,25 +253,19 @@ __device__ __forceinline__ bool aff_load(Aff<F> &a, const uint32_t *__restrict__
 // reference-form affine point (x || y, N64 u64 each) -> internal-form storage
 template <class F>
 __device__ __forceinline__ void aff_ref_to_int(uint32_t *__restrict__ out, const uint64_t *__restrict__ in) {
-  const uint4 *q = reinterpret_cast<const uint4 *>(in);
-  uint32_t all = 0xffffffffu;
-  uint32_t w[2 * F::NW];
+  uint64_t all = ~0ull;
 #pragma unroll
-  for (int i = 0; i < F::NW / 2; i++) {
-    uint4 x = q[i];
-    w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
-    all &= x.x & x.y & x.z & x.w;
-  }
-  if (all == 0xffffffffu) {
+  for (int i = 0; i < 2 * F::N64; i++) all &= in[i];
+  if (all == ~0ull) {
     uint4 *o = reinterpret_cast<uint4 *>(out);
 #pragma unroll
     for (int i = 0; i < F::SN / 2; i++) o[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     return;
   }
   Fe<F> x, y, t;
-  fe_unpack(t, w);
+  fe_load_ref(t, in);
   fe_to_int(x, t);
-  fe_unpack(t, w + F::NW);
+  fe_load_ref(t, in + F::N64);
   fe_to_int(y, t);
   fe_store_u(out, x);
   fe_store_u(out + F::SN, y);

@@ -167,6 +167,84 @@ template <class F> inline void inv(Fe<F> &r, const Fe<F> &a) {
 }
 
 // ---------------------------------------------------------------------------
+// Fp2 = Fp[u]/(u^2 + 1) (both curves; <C>_Fp2_mont.c:183-215): an element is c0 || c1,
+// N64 limbs each, exactly the reference layout.  Overloads below are picked over the
+// generic templates by partial ordering, so Proj / Xyzz code instantiates on Fp2.
+template <class B>
+struct HF2 {
+  using Base = B;
+  static constexpr int N = 2 * B::N;
+};
+template <class B> inline void f2s(Fe<B> &c0, Fe<B> &c1, const Fe<HF2<B>> &a) {
+  memcpy(c0.v, a.v, sizeof c0.v);
+  memcpy(c1.v, a.v + B::N, sizeof c1.v);
+}
+template <class B> inline void f2j(Fe<HF2<B>> &r, const Fe<B> &c0, const Fe<B> &c1) {
+  memcpy(r.v, c0.v, sizeof c0.v);
+  memcpy(r.v + B::N, c1.v, sizeof c1.v);
+}
+template <class B> inline void set_one(Fe<HF2<B>> &r) {
+  Fe<B> o, z;
+  set_one(o);
+  set_zero(z);
+  f2j(r, o, z);
+}
+template <class B> inline bool is_one(const Fe<HF2<B>> &a) {
+  Fe<B> a0, a1;
+  f2s(a0, a1, a);
+  return is_one(a0) && is_zero(a1);
+}
+template <class B> inline void add(Fe<HF2<B>> &r, const Fe<HF2<B>> &a, const Fe<HF2<B>> &b) {
+  Fe<B> a0, a1, b0, b1;
+  f2s(a0, a1, a);
+  f2s(b0, b1, b);
+  add(a0, a0, b0);
+  add(a1, a1, b1);
+  f2j(r, a0, a1);
+}
+template <class B> inline void sub(Fe<HF2<B>> &r, const Fe<HF2<B>> &a, const Fe<HF2<B>> &b) {
+  Fe<B> a0, a1, b0, b1;
+  f2s(a0, a1, a);
+  f2s(b0, b1, b);
+  sub(a0, a0, b0);
+  sub(a1, a1, b1);
+  f2j(r, a0, a1);
+}
+template <class B> inline void neg(Fe<HF2<B>> &r, const Fe<HF2<B>> &a) {
+  Fe<HF2<B>> z;
+  set_zero(z);
+  sub(r, z, a);
+}
+template <class B> inline void mul(Fe<HF2<B>> &r, const Fe<HF2<B>> &a, const Fe<HF2<B>> &b) {
+  Fe<B> a0, a1, b0, b1, t0, t1, s, u;
+  f2s(a0, a1, a);
+  f2s(b0, b1, b);
+  mul(t0, a0, b0);
+  mul(t1, a1, b1);
+  add(s, a0, a1);
+  add(u, b0, b1);
+  mul(s, s, u);
+  sub(s, s, t0);
+  sub(s, s, t1);
+  sub(t0, t0, t1);
+  f2j(r, t0, s);
+}
+template <class B> inline void sqr(Fe<HF2<B>> &r, const Fe<HF2<B>> &a) { mul(r, a, a); }
+// 1/(a0 + a1 u) = (a0 - a1 u) / (a0^2 + a1^2); 0 -> 0
+template <class B> inline void inv(Fe<HF2<B>> &r, const Fe<HF2<B>> &a) {
+  Fe<B> a0, a1, n, t;
+  f2s(a0, a1, a);
+  mul(n, a0, a0);
+  mul(t, a1, a1);
+  add(n, n, t);
+  inv(n, n);
+  mul(a0, a0, n);
+  mul(a1, a1, n);
+  neg(a1, a1);
+  f2j(r, a0, a1);
+}
+
+// ---------------------------------------------------------------------------
 // G1 in homogeneous projective coordinates (x = X/Z, y = Y/Z), a = 0.
 // Infinity: Z == 0 (canonical form (0 : 1 : 0), reference set_infinity
 // bls12_381_G1_proj.c:179-183).  Affine infinity: all-0xFF bytes (G1_affine.c:1-6).

@@ -18,6 +18,15 @@ template <> struct HostOf<BLS381> {
   static void b3(zkh::Fe<Fp> &r) { const uint64_t v[] = ZK_BLS12_381_B3_FP64; memcpy(r.v, v, sizeof r.v); }
 };
 
+template <> struct HostOf<BN254_G2> {
+  using Fp = zkh::HF2<zkh::BN_Fp>;
+  using Fr = zkh::BN_Fr;
+};
+template <> struct HostOf<BLS381_G2> {
+  using Fp = zkh::HF2<zkh::BLS_Fp>;
+  using Fr = zkh::BLS_Fr;
+};
+
 int msm_default_window(int n);
 
 // scalars: n x nl u64 (nl in 1..4) (Montgomery Fr if mont, else plain 256-bit integers)

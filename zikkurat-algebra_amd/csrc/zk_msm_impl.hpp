@@ -1,0 +1,774 @@
+#pragma once
+// zk_msm_impl.hpp -- (template bodies; instantiated in zk_msm.hip / zk_msm_g2.hip) Pippenger bucket MSM for G1 (BN128 and BLS12-381) on gfx950.
+//
+// Replaces <C>_G1_proj_MSM_std_coeff_proj_out_variable (bls12_381_G1_proj.c:507-587)
+// and its callers (:597-670).  Same mathematical result (sum_i k_i * P_i with the
+// 256-bit scalars used verbatim -- no reduction mod r, no GLV, so the result is
+// identical for points outside the order-r subgroup too), computed with
+// a GPU-shaped schedule:
+//
+//   0. k_points_int affine points -> internal radix (one product per coordinate)
+//   1. k_digits     scalar (Montgomery -> standard by REDC, Fr_mont.c:330-335) ->
+//                   signed c-bit digits for all W windows -> (key, index|sign), key =
+//                   window << c | (|digit| - 1); keys are emitted window-major
+//   2. sort         LSD radix sort of the W*n pairs on the c in-window bits only
+//                   (hipCUB onesweep, 2 passes at c = 16): the sort is stable, so
+//                   equal digits stay window-major and every (window, digit) bucket is
+//                   one contiguous run, ordered by rank = digit * W + window
+//   3. k_offsets    bucket start offsets (per rank) from the sorted keys
+//   4. k_accum      balanced bucket accumulation: every thread adds exactly CH
+//                   consecutive sorted entries (mixed XYZZ += affine adds), flushing
+//                   complete runs to their bucket and boundary runs as partial items
+//   5. k_stitch     partial items are compacted and summed per bucket with the same
+//                   balanced scheme, level after level (log_{SCH/2} levels): no serial
+//                   loop anywhere, so skewed scalars (all equal, carry windows) stay fast
+//   6. k_seg        per (window, segment of L buckets): T = sum B_m, R = sum (m-lo+1) B_m
+//   7. k_jobsum     sum_m m B_m = sum_s R_s + L * sum_k 2^k U_k, U_k = sum_{s: bit k} T_s:
+//                   every term is a plain point sum; one workgroup per (window, job)
+//                   with an LDS tree
+//   9. host         Horner over the power-of-two exponents, normalise / to_affine
+//
+// Every phase is wide (>= ~1e5 threads at 2^20) except the last tiny levels: a lone
+// wavefront's serial chain of 381-bit point adds is slow on CDNA4, so the
+// deep-but-narrow tail runs on one host core (step 9).
+#include <hipcub/hipcub.hpp>
+#include <chrono>
+#include <vector>
+#include "zk_curve.hpp"
+#include "zk_host.hpp"
+#include "zk_runtime.hpp"
+#include "zk_msm.hpp"
+
+namespace zk {
+
+// ---------------------------------------------------------------------------
+// XYZZ storage: 4 consecutive field elements, F::N u32 words each.
+template <class F>
+__device__ __forceinline__ void xyzz_store(uint32_t *p, const Xyzz<F> &a) {
+  fe_store_u(p + 0 * F::SN, a.X);
+  fe_store_u(p + 1 * F::SN, a.Y);
+  fe_store_u(p + 2 * F::SN, a.ZZ);
+  fe_store_u(p + 3 * F::SN, a.ZZZ);
+}
+template <class F>
+__device__ __forceinline__ void xyzz_load(Xyzz<F> &a, const uint32_t *p) {
+  fe_load_u(a.X, p + 0 * F::SN);
+  fe_load_u(a.Y, p + 1 * F::SN);
+  fe_load_u(a.ZZ, p + 2 * F::SN);
+  fe_load_u(a.ZZZ, p + 3 * F::SN);
+}
+template <class F>
+constexpr int xyzz_words() { return 4 * F::SN; }
+template <class F>
+constexpr int aff_words() { return 2 * F::SN; }
+
+// 0. affine points: reference form -> internal form (once per call)
+template <class C>
+__global__ void __launch_bounds__(256) k_points_int(const uint64_t *__restrict__ pts, int n,
+                                                    uint32_t *__restrict__ out) {
+  using F = typename C::Fp;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  aff_ref_to_int<F>(out + (size_t)i * aff_words<F>(), pts + (size_t)i * 2 * F::N64);
+}
+
+// ---------------------------------------------------------------------------
+// 1. digits -> (key, value) pairs for the bucket sort.
+//    key = w << c | (|digit| - 1), or w << c | B (sorts after every digit) for a zero
+//    digit; value = point index | sign << 31
+template <class C>
+__global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int nl, int mont,
+                                                int c, int W, uint32_t *__restrict__ keys,
+                                                uint32_t *__restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  using Fr = typename C::Fr;
+  uint32_t k[9];
+  {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // std scalars of 1..3 limbs: zero-extended
+      const uint64_t w = (j < nl) ? scalars[(size_t)i * nl + j] : 0;
+      k[2 * j] = (uint32_t)w;
+      k[2 * j + 1] = (uint32_t)(w >> 32);
+    }
+    k[8] = 0;
+    if (mont) {  // Montgomery -> standard (REDC), Fr_mont.c:330-335
+      Fe<Fr> s, t;
+      fe_unpack(s, k);
+      fe_ref_to_std(t, s);
+      fe_pack(k, t);
+    }
+  }
+  const uint32_t B = 1u << (c - 1);
+  const uint32_t full = 1u << c;
+  const uint32_t mask = full - 1;
+  uint32_t carry = 0;
+  for (int w = 0; w < W; w++) {
+    uint32_t raw = (k[0] & mask) + carry;
+    // shift the 256-bit scalar right by c (c < 32)
+#pragma unroll
+    for (int j = 0; j < 8; j++) k[j] = __builtin_amdgcn_alignbit(k[j + 1], k[j], c);
+    uint32_t mag, sign;
+    if (raw > B) {  // negative digit raw - 2^c (zero when raw == 2^c)
+      mag = full - raw;
+      sign = 0x80000000u;
+      carry = 1;
+    } else {
+      mag = raw;
+      sign = 0;
+      carry = 0;
+    }
+    keys[(size_t)w * n + i] = ((uint32_t)w << c) | (mag ? mag - 1 : B);
+    vals[(size_t)w * n + i] = (uint32_t)i | sign;
+  }
+}
+
+// 3. bucket offsets from the sorted keys: offsets[b] = first position whose rank is
+//    >= b, rank = digit * W + window (zero digits rank >= nb), one binary search per
+//    bucket (no serial loops, whatever the key distribution)
+__device__ __forceinline__ uint32_t key_rank(uint32_t key, int c, uint32_t W) {
+  return (key & ((1u << c) - 1)) * W + (key >> c);
+}
+// storage slot of the bucket with rank b (window-major: w * B + digit)
+__device__ __forceinline__ uint32_t bucket_slot(uint32_t b, uint32_t W, uint32_t B) {
+  return (b % W) * B + b / W;
+}
+static __global__ void __launch_bounds__(256) k_offsets(const uint32_t *__restrict__ skeys, uint32_t M, uint32_t nb,
+                                                 int c, uint32_t W, uint32_t *__restrict__ offsets) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nb) return;
+  uint32_t lo = 0, hi = M;  // first index in [lo, hi] with rank >= b
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (key_rank(skeys[mid], c, W) < b) lo = mid + 1; else hi = mid;
+  }
+  offsets[b] = lo;
+}
+
+// first bucket index b with offsets[b+1] > e  (offsets has nb+1 entries)
+__device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ offsets, uint32_t nb, uint32_t e) {
+  uint32_t lo = 0, hi = nb;  // answer in [lo, hi)
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (offsets[mid] <= e) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+template <class F>
+__device__ __forceinline__ void load_signed_point(Aff<F> &a, bool &inf, const uint32_t *__restrict__ points,
+                                                  uint32_t code) {
+  const uint32_t idx = code & 0x7fffffffu;
+  inf = !aff_load(a, points + (size_t)idx * aff_words<F>());
+  if (!inf && (code & 0x80000000u)) {
+    Fe<F> ny;
+    fe_neg(ny, a.y);
+    a.y = ny;
+  }
+}
+
+// 4. level-0 balanced accumulation: thread t owns sorted entries [t*CH, min((t+1)*CH, total)).
+//    Runs of one bucket that lie entirely inside the chunk are written straight to
+//    buckets[b]; a run that crosses the chunk boundary (the chunk's first and/or last run)
+//    becomes a "partial item" (key b, XYZZ sum) in slot 2t / 2t+1 of the item arrays.
+//    Item slots that stay empty carry key = nb (dropped by the compaction).
+template <class C>
+__global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ points,
+                                               const uint32_t *__restrict__ list,
+                                               const uint32_t *__restrict__ offsets, uint32_t nb,
+                                               int CH, uint32_t W, uint32_t B, uint32_t *__restrict__ buckets,
+                                               uint32_t *__restrict__ ikeys, uint32_t *__restrict__ ivals,
+                                               uint32_t nslots) {
+  using F = typename C::Fp;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * t >= nslots) return;
+  const uint32_t total = offsets[nb];
+  const uint32_t cs = t * (uint32_t)CH;
+  uint32_t k0 = nb, k1 = nb;  // item keys of slots 2t, 2t+1
+  if (cs < total) {
+    const uint32_t ce = min(total, cs + (uint32_t)CH);
+    uint32_t b = bucket_of(offsets, nb, cs);
+    uint32_t bbeg = offsets[b], bend = offsets[b + 1];
+    bool first_run = true;
+    Xyzz<F> acc;
+    xyzz_set_inf(acc);
+    for (uint32_t e = cs; e < ce; e++) {
+      if (e >= bend) {  // run of bucket b ends inside the chunk
+        xyzz_settle(acc);
+        if (first_run && bbeg < cs) {
+          xyzz_store(ivals + (size_t)(2 * t) * xyzz_words<F>(), acc);
+          k0 = b;
+        } else {
+          xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
+        }
+        first_run = false;
+        xyzz_set_inf(acc);
+        do { b++; bbeg = offsets[b]; bend = offsets[b + 1]; } while (bend <= e);
+      }
+      Aff<F> P;
+      bool inf;
+      load_signed_point(P, inf, points, list[e]);
+      if (!inf) xyzz_acc_aff(acc, P);
+    }
+    // last run: partial if it started before the chunk or continues after it
+    xyzz_settle(acc);
+    if (bbeg < cs || bend > ce) {
+      const uint32_t slot = first_run ? 2 * t : 2 * t + 1;
+      xyzz_store(ivals + (size_t)slot * xyzz_words<F>(), acc);
+      if (first_run) k0 = b; else k1 = b;
+    } else {
+      xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
+    }
+  }
+  ikeys[2 * t] = k0;
+  ikeys[2 * t + 1] = k1;
+}
+
+// 5a. compaction of the partial items (keys < nb), order preserving: scatter by a
+//     prefix sum of the valid flags (scan done by hipCUB on `flags`)
+static __global__ void __launch_bounds__(256) k_item_flags(const uint32_t *__restrict__ ikeys, const uint32_t *__restrict__ count,
+                                                    uint32_t nslots_max, uint32_t nb, uint32_t *__restrict__ flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots_max) return;
+  const uint32_t n = count ? *count : nslots_max;
+  flags[i] = (i < n && ikeys[i] < nb) ? 1u : 0u;
+}
+template <class C>
+__global__ void __launch_bounds__(256) k_item_compact(const uint32_t *__restrict__ ikeys, const uint32_t *__restrict__ ivals,
+                                                      const uint32_t *__restrict__ flags, const uint32_t *__restrict__ pos,
+                                                      uint32_t nslots_max, uint32_t *__restrict__ okeys,
+                                                      uint32_t *__restrict__ ovals, uint32_t *__restrict__ ocount) {
+  using F = typename C::Fp;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots_max) return;
+  if (i == nslots_max - 1) *ocount = pos[i] + flags[i];
+  if (!flags[i]) return;
+  const uint32_t o = pos[i];
+  okeys[o] = ikeys[i];
+  const uint4 *s = reinterpret_cast<const uint4 *>(ivals + (size_t)i * xyzz_words<F>());
+  uint4 *d = reinterpret_cast<uint4 *>(ovals + (size_t)o * xyzz_words<F>());
+#pragma unroll
+  for (int q = 0; q < xyzz_words<F>() / 4; q++) d[q] = s[q];
+}
+
+// 5b. stitch level: the compacted items (sorted by key) are summed per key with the
+//     same balanced-chunk scheme; complete runs go to buckets[b], runs crossing a chunk
+//     boundary become the next level's items.  Levels repeat until one chunk remains.
+template <class C>
+__global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                const uint32_t *__restrict__ count, uint32_t nb, int CH,
+                                                uint32_t W, uint32_t B, uint32_t *__restrict__ buckets, uint32_t *__restrict__ okeys,
+                                                uint32_t *__restrict__ ovals, uint32_t nslots) {
+  using F = typename C::Fp;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * t >= nslots) return;
+  const uint32_t M = *count;
+  const uint32_t cs = t * (uint32_t)CH;
+  uint32_t k0 = nb, k1 = nb;
+  if (cs < M) {
+    const uint32_t ce = min(M, cs + (uint32_t)CH);
+    uint32_t b = keys[cs];
+    const bool cont_in = cs > 0 && keys[cs - 1] == b;
+    bool first_run = true;
+    Xyzz<F> acc;
+    xyzz_set_inf(acc);
+    for (uint32_t e = cs; e < ce; e++) {
+      const uint32_t k = keys[e];
+      if (k != b) {
+        if (first_run && cont_in) {
+          xyzz_store(ovals + (size_t)(2 * t) * xyzz_words<F>(), acc);
+          k0 = b;
+        } else {
+          xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
+        }
+        first_run = false;
+        xyzz_set_inf(acc);
+        b = k;
+      }
+      Xyzz<F> v;
+      xyzz_load(v, vals + (size_t)e * xyzz_words<F>());
+      xyzz_add(acc, v);
+    }
+    const bool cont_out = ce < M && keys[ce] == b;
+    if ((first_run && cont_in) || cont_out) {
+      const uint32_t slot = first_run ? 2 * t : 2 * t + 1;
+      xyzz_store(ovals + (size_t)slot * xyzz_words<F>(), acc);
+      if (first_run) k0 = b; else k1 = b;
+    } else {
+      xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
+    }
+  }
+  okeys[2 * t] = k0;
+  okeys[2 * t + 1] = k1;
+}
+
+// In-wavefront segmented point sum: the G lanes of an aligned segment (G a power of two
+// <= 64) fold their accumulators with log2(G) cross-lane steps; lane 0 of the segment
+// ends up with the segment's sum.  (Every lane executes every step, so the cost is
+// log2(G) point adds of latency whatever the segment size.)
+template <class F>
+__device__ __forceinline__ Xyzz<F> xyzz_shfl_down(const Xyzz<F> &a, int off, int width) {
+  Xyzz<F> r;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {
+    r.X.v[i] = (uint32_t)__shfl_down((int)a.X.v[i], off, width);
+    r.Y.v[i] = (uint32_t)__shfl_down((int)a.Y.v[i], off, width);
+    r.ZZ.v[i] = (uint32_t)__shfl_down((int)a.ZZ.v[i], off, width);
+    r.ZZZ.v[i] = (uint32_t)__shfl_down((int)a.ZZZ.v[i], off, width);
+  }
+  return r;
+}
+template <class F>
+__device__ __forceinline__ void seg_fold(Xyzz<F> &acc, int G) {
+  for (int off = G >> 1; off >= 1; off >>= 1) {
+    Xyzz<F> o = xyzz_shfl_down(acc, off, G);
+    xyzz_add(acc, o);
+  }
+}
+
+// Segment layout shared by the two reduction kernels: per window, segments of
+// decreasing size G (aligned by construction), the window's lane block padded to a
+// multiple of 64 so no wavefront spans two windows.
+struct SegRegion {
+  int count;  // segments in this region
+  int G;      // lanes per segment
+  int len;    // items per segment
+};
+
+// 6. digit split of the bucket weights.  Bucket m of a window (digit m + 1) has
+//    m = m1 * 2^l0 + m0 (l0 + l1 = c - 1), so
+//       sum_m (m+1) B_m = sum_v v Y0_v + 2^l0 sum_v v Y1_v + sum_v Y0_v,
+//       Y0_v = sum_{m0 = v} B_m (2^l1 buckets),  Y1_v = sum_{m1 = v} B_m (2^l0 buckets).
+//    Every Y is a PLAIN sum (no weights, no running-sum chain): G lanes per Y, each adds
+//    len/G buckets, then an in-wavefront fold.  Region 0: the 2^l1 sums Y1 (longer
+//    segments first), region 1: the 2^l0 sums Y0.  Output Y[w][y]: y < 2^l0 -> Y0_y,
+//    else Y1_(y - 2^l0).
+template <class C>
+__global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ buckets,
+                                              const uint32_t *__restrict__ offsets, int W, int c, int l0,
+                                              SegRegion r0, SegRegion r1, int wlanes,
+                                              uint32_t *__restrict__ Y) {
+  using F = typename C::Fp;
+  const int l1 = c - 1 - l0;
+  const int NY = (1 << l0) + (1 << l1);
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int w = g / wlanes, t = g % wlanes;  // W * wlanes is a multiple of 256 by launch
+  const bool active = w < W;
+  const int n0 = r0.count * r0.G;
+  int G, len, seg, lane;
+  bool hiY;  // Y1 (region 0) or Y0 (region 1)
+  if (t < n0) { G = r0.G; len = r0.len; seg = t / G; lane = t % G; hiY = true; }
+  else if (t < n0 + r1.count * r1.G) { G = r1.G; len = r1.len; seg = (t - n0) / G; lane = (t - n0) % G; hiY = false; }
+  else { G = 1; len = 0; seg = 0; lane = 0; hiY = false; }  // padding lanes: no fold
+  const uint32_t B = 1u << (c - 1);
+  const int per = len / G;
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  if (active) {
+    for (int k = 0; k < per; k++) {
+      const int s = lane * per + k;
+      const uint32_t m = hiY ? ((uint32_t)seg << l0) + s : ((uint32_t)s << l0) + seg;
+      const uint32_t rank = m * (uint32_t)W + (uint32_t)w;
+      if (offsets[rank + 1] > offsets[rank]) {  // empty buckets hold garbage (never written)
+        Xyzz<F> bm;
+        xyzz_load(bm, buckets + ((size_t)w * B + m) * xyzz_words<F>());
+        xyzz_add(acc, bm);
+      }
+    }
+  }
+  seg_fold(acc, G);
+  if (active && lane == 0 && len > 0) {
+    const int y = hiY ? (1 << l0) + seg : seg;
+    xyzz_store(Y + ((size_t)w * NY + y) * xyzz_words<F>(), acc);
+  }
+}
+
+// 7. weighted sums of the Y's by bits: per window, job (d, b) for b < l_d is
+//    U_{d,b} = sum_{v: bit b of v} Yd_v (2^(l_d - 1) items) and one job is sum_v Y0_v
+//    (2^l0 items); J = l0 + l1 + 1 = c jobs.  Same segment scheme: jobs ordered by
+//    length (total, then the l0 jobs over Y0, then the l1 jobs over Y1), G lanes each.
+//    Output P[w][j]: j = 0 total, 1..l0 -> (0, j-1), l0+1.. -> (1, j-1-l0).
+template <class C>
+__global__ void __launch_bounds__(256) k_jobsum(const uint32_t *__restrict__ Y, int W, int c, int l0, int QA,
+                                                int wlanes, uint32_t *__restrict__ out) {
+  using F = typename C::Fp;
+  const int l1 = c - 1 - l0;
+  const int NY = (1 << l0) + (1 << l1);
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int w = g / wlanes, t = g % wlanes;
+  const bool active = w < W;
+  // job j: length n_j, segment size G_j = clamp(n_j / QA, 1, 64); lane offset = prefix sum
+  int j = -1, G = 1, lane = 0, off = 0;  // padding lanes: no job, no fold
+  for (int jj = 0; jj < c; jj++) {
+    const int n = jj == 0 ? (1 << l0) : (jj <= l0 ? (1 << (l0 - 1)) : (1 << (l1 - 1)));
+    int Gj = n / QA;
+    Gj = Gj < 1 ? 1 : (Gj > 64 ? 64 : Gj);
+    if (t >= off && t < off + Gj) { j = jj; G = Gj; lane = t - off; }
+    off += Gj;
+  }
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  if (active && j >= 0) {
+    const int d = (j == 0 || j <= l0) ? 0 : 1;
+    const int b = j == 0 ? -1 : (d == 0 ? j - 1 : j - 1 - l0);
+    const int ld = d ? l1 : l0;
+    const int n = (b < 0) ? (1 << ld) : (1 << (ld - 1));
+    const int per = n / G;
+    const uint32_t *Yd = Y + ((size_t)w * NY + (d ? (1 << l0) : 0)) * xyzz_words<F>();
+    for (int k = 0; k < per; k++) {
+      const int e = lane * per + k;
+      int v = e;
+      if (b >= 0) {
+        const int lowmask = (1 << b) - 1;
+        v = ((e & ~lowmask) << 1) | (1 << b) | (e & lowmask);
+      }
+      Xyzz<F> p;
+      xyzz_load(p, Yd + (size_t)v * xyzz_words<F>());
+      xyzz_add(acc, p);
+    }
+  }
+  seg_fold(acc, G);
+  if (active && j >= 0 && lane == 0) xyzz_store(out + ((size_t)w * c + j) * xyzz_words<F>(), acc);
+}
+
+// export: XYZZ (device form) -> canonical reference-form coordinates, 4 x NP64 u64
+template <class C>
+__global__ void k_export(const uint32_t *__restrict__ in, int n, uint64_t *__restrict__ out) {
+  using F = typename C::Fp;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  Xyzz<F> p;
+  xyzz_load(p, in + (size_t)g * xyzz_words<F>());
+  uint64_t *o = out + (size_t)g * 4 * F::N64;
+  Fe<F> t;
+  fe_to_ref(t, p.X);
+  fe_store_ref(o + 0 * F::N64, t);
+  fe_to_ref(t, p.Y);
+  fe_store_ref(o + 1 * F::N64, t);
+  fe_to_ref(t, p.ZZ);
+  fe_store_ref(o + 2 * F::N64, t);
+  fe_to_ref(t, p.ZZZ);
+  fe_store_ref(o + 3 * F::N64, t);
+}
+
+// ---------------------------------------------------------------------------
+// host orchestration
+
+struct MsmShape {
+  int n, c, W, B, l0, l1, NY, QY, J, CH, SCH, QA;
+  SegRegion r0, r1;
+  int ylanes, jlanes;  // lanes per window of k_ysum / k_jobsum (multiples of 64)
+};
+
+static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; return r; }
+
+static int env_int(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+
+// bits: bit length bound of the scalars (255/254 for canonical Montgomery-path scalars
+// after REDC, 64*nl for std scalars, which are used verbatim).  Signed digits need
+// floor(bits/c) + 1 windows: the top window then holds at most c-1 bits plus the carry,
+// i.e. a digit <= 2^(c-1) = B, so no carry leaves it.
+static MsmShape make_shape(int n, int c, int bits) {
+  static const int envQY = env_int("ZK_MSM_QY", 0), envQA = env_int("ZK_MSM_QA", 0);
+  MsmShape s;
+  s.n = n;
+  s.c = c;
+  s.W = bits / c + 1;
+  s.B = 1 << (c - 1);
+  s.l0 = c / 2;  // l0 + l1 = c - 1, l0 >= l1
+  s.l1 = c - 1 - s.l0;
+  s.NY = (1 << s.l0) + (1 << s.l1);
+  auto pow2 = [](int v) { int r = 1; while (2 * r <= v) r *= 2; return r; };  // segments need powers of 2
+  s.QY = envQY > 0 ? pow2(envQY) : 16;  // buckets per lane in the Y sums (swept on MI355X)
+  auto clampG = [](int g) { return g < 1 ? 1 : (g > 64 ? 64 : g); };
+  s.r0 = SegRegion{1 << s.l1, clampG((1 << s.l0) / s.QY), 1 << s.l0};  // Y1 sums
+  s.r1 = SegRegion{1 << s.l0, clampG((1 << s.l1) / s.QY), 1 << s.l1};  // Y0 sums
+  s.ylanes = (s.r0.count * s.r0.G + s.r1.count * s.r1.G + 63) & ~63;
+  s.J = c;
+  s.CH = 64;   // entries per thread in the level-0 accumulation
+  s.SCH = 8;   // items per thread in the stitch levels (mostly pairs: keep it wide)
+  s.QA = envQA > 0 ? pow2(envQA) : 8;  // items per lane in the weighted job sums
+  s.jlanes = 0;
+  for (int j = 0; j < c; j++) {  // same job order / sizes as k_jobsum
+    const int n = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
+    s.jlanes += clampG(n / s.QA);
+  }
+  s.jlanes = (s.jlanes + 63) & ~63;
+  return s;
+}
+
+static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.n + s.CH - 1) / s.CH); }
+static size_t stitch_slots1(const MsmShape &s) { return 2 * ((stitch_slots0(s) + s.SCH - 1) / s.SCH) + 2; }
+
+template <class C>
+static size_t workspace_bytes(const MsmShape &s) {
+  using F = typename C::Fp;
+  const size_t xw = xyzz_words<F>() * 4;  // bytes per XYZZ
+  const size_t nb = (size_t)s.W * s.B;
+  const size_t maxent = (size_t)s.W * s.n;
+  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s);
+  size_t cub = 0, cub2 = 0;
+  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                              (uint32_t *)nullptr, (uint32_t *)nullptr, (int)maxent, 0, s.c));
+  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)ns0));
+  size_t bytes = 0;
+  auto add = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
+  add((size_t)s.n * 4 * 8);               // staged scalars (<= 4 limbs)
+  add((size_t)s.n * 2 * C::NP64 * 8);     // staged points
+  add((size_t)s.n * aff_words<F>() * 4);  // internal-form points
+  add(maxent * 4 * 4);                    // keys, vals, sorted keys, sorted vals
+  add((nb + 1) * 4);                      // offsets
+  add(ns0 * (xw + 4) * 2 + ns0 * 8 + 64); // level-0 items, compacted items, flags, pos, count
+  add(ns1 * (xw + 4) * 2);                // stitch ping-pong
+  add(nb * xw);                           // buckets
+  add((size_t)s.W * s.NY * xw);              // Y
+  add((size_t)s.W * s.J * xw);               // per-(window, job) sums
+  add((size_t)s.W * s.J * 4 * C::NP64 * 8);    // export
+  add(cub > cub2 ? cub : cub2);
+  return bytes + (1 << 20);
+}
+
+// opt-in phase profile (env ZK_MSM_PROFILE=1): HIP events between the phases of one
+// call, printed to stderr with the host-side finish time.  Off by default.
+struct PhaseProf {
+  bool on = false;
+  hipStream_t st = nullptr;
+  std::vector<std::pair<const char *, hipEvent_t>> ev;
+  explicit PhaseProf(hipStream_t s) : st(s) {
+    static const int enabled = env_int("ZK_MSM_PROFILE", 0);
+    on = enabled != 0;
+    mark("start");
+  }
+  void mark(const char *name) {
+    if (!on) return;
+    hipEvent_t e;
+    ZK_CHECK(hipEventCreate(&e));
+    ZK_CHECK(hipEventRecord(e, st));
+    ev.emplace_back(name, e);
+  }
+  void report(double host_ms) {
+    if (!on) return;
+    ZK_CHECK(hipStreamSynchronize(st));
+    fprintf(stderr, "[zk msm]");
+    for (size_t i = 1; i < ev.size(); i++) {
+      float ms = 0;
+      ZK_CHECK(hipEventElapsedTime(&ms, ev[i - 1].second, ev[i].second));
+      fprintf(stderr, " %s=%.3f", ev[i].first, ms);
+    }
+    fprintf(stderr, " host_finish=%.3f ms\n", host_ms);
+    for (auto &e : ev) ZK_CHECK(hipEventDestroy(e.second));
+    ev.clear();
+  }
+};
+
+template <class C>
+static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<typename HostOf<C>::Fp> &out);
+
+// Run the device pipeline. scalars/points are DEVICE pointers (or host pointers when
+// host_inputs, in which case they are staged).  Result: projective point in
+// reference Montgomery form (not normalised), written to `out`.
+template <class C>
+static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs,
+                    bool mont, int window, zkh::Proj<typename HostOf<C>::Fp> &out) {
+  using HF = typename HostOf<C>::Fp;
+  using F = typename C::Fp;
+  if (n <= 0) {
+    zkh::proj_set_inf<HF>(out);
+    return;
+  }
+  const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
+  ZK_REQUIRE(nl >= 1 && nl <= 4, "msm: expo_nlimbs must be in 1..4 (scalars up to 256 bits)");
+  ZK_REQUIRE(!mont || nl == 4, "msm: Montgomery coefficients must have expo_nlimbs == 4");
+  MsmShape s = make_shape(n, c, mont ? HostOf<C>::Fr::BITS : 64 * nl);
+  const size_t nb = (size_t)s.W * s.B;
+  const size_t xw = xyzz_words<F>();
+  hipStream_t st = dev.stream;
+
+  dev.arena.reserve(workspace_bytes<C>(s));
+  dev.arena.reset();
+  const uint64_t *d_sc = scalars, *d_pt = points;
+  if (host_inputs) {
+    uint64_t *a = dev.arena.take<uint64_t>((size_t)n * nl);
+    uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
+    ZK_CHECK(hipMemcpyAsync(a, scalars, (size_t)n * nl * 8, hipMemcpyHostToDevice, st));
+    ZK_CHECK(hipMemcpyAsync(b, points, (size_t)n * 2 * C::NP64 * 8, hipMemcpyHostToDevice, st));
+    d_sc = a;
+    d_pt = b;
+  }
+  uint32_t *pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
+  const size_t maxent = (size_t)s.W * n;
+  uint32_t *keys = dev.arena.take<uint32_t>(maxent);
+  uint32_t *vals = dev.arena.take<uint32_t>(maxent);
+  uint32_t *skeys = dev.arena.take<uint32_t>(maxent);
+  uint32_t *list = dev.arena.take<uint32_t>(maxent);  // sorted values
+  uint32_t *offsets = dev.arena.take<uint32_t>(nb + 1);
+  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s);
+  uint32_t *ikeys0 = dev.arena.take<uint32_t>(ns0);
+  uint32_t *ivals0 = dev.arena.take<uint32_t>(ns0 * xw);
+  uint32_t *ckeys = dev.arena.take<uint32_t>(ns0);
+  uint32_t *cvals = dev.arena.take<uint32_t>(ns0 * xw);
+  uint32_t *flags = dev.arena.take<uint32_t>(ns0);
+  uint32_t *pos = dev.arena.take<uint32_t>(ns0);
+  uint32_t *ccount = dev.arena.take<uint32_t>(16);
+  uint32_t *okA = dev.arena.take<uint32_t>(ns1);
+  uint32_t *ovA = dev.arena.take<uint32_t>(ns1 * xw);
+  uint32_t *okB = dev.arena.take<uint32_t>(ns1);
+  uint32_t *ovB = dev.arena.take<uint32_t>(ns1 * xw);
+  uint32_t *buckets = dev.arena.take<uint32_t>(nb * xw);
+  uint32_t *Y = dev.arena.take<uint32_t>((size_t)s.W * s.NY * xw);
+  uint32_t *P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * xw);
+  uint64_t *exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
+  size_t cub = 0, cub2 = 0;
+  const int kbits = c;  // in-window digit bits only (see step 2)
+  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
+  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
+  if (cub2 > cub) cub = cub2;
+  void *cubtmp = dev.arena.take<char>(cub);
+
+  PhaseProf prof(st);
+  hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_pt, n, pts_int);
+  ZK_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_sc, n, nl, mont ? 1 : 0, c, s.W,
+                     keys, vals);
+  ZK_CHECK(hipGetLastError());
+  prof.mark("digits");
+  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
+  prof.mark("sort");
+  hipLaunchKernelGGL(k_offsets, dim3(div_up(nb + 1, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
+                     (uint32_t)nb, c, (uint32_t)s.W, offsets);
+  ZK_CHECK(hipGetLastError());
+
+  prof.mark("offsets");
+  KernelTimer &kt = dominant_timer();
+  {
+    if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev0, st));
+    // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
+    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(ns0 / 2, 256)), dim3(256), 0, st, pts_int, list, offsets,
+                       (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0, ivals0, (uint32_t)ns0);
+    ZK_CHECK(hipGetLastError());
+    if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev1, st));
+  }
+  prof.mark("accum");
+  // stitch levels: compact the partial items, sum them per bucket, repeat
+  {
+    const uint32_t *inK = ikeys0, *inV = ivals0;
+    const uint32_t *inCount = nullptr;  // level 0: every slot is examined
+    size_t slots = ns0;
+    uint32_t *outK = okA, *outV = ovA, *altK = okB, *altV = ovB;
+    for (;;) {
+      hipLaunchKernelGGL(k_item_flags, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, inCount, (uint32_t)slots,
+                         (uint32_t)nb, flags);
+      ZK_CHECK(hipGetLastError());
+      size_t cb = cub;
+      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, flags, pos, (int)slots, st));
+      hipLaunchKernelGGL(k_item_compact<C>, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, inV, flags, pos,
+                         (uint32_t)slots, ckeys, cvals, ccount);
+      ZK_CHECK(hipGetLastError());
+      const bool final_level = slots <= (size_t)s.SCH;  // all items fit one chunk: everything completes
+      const size_t nout = final_level ? 2 : 2 * ((slots + s.SCH - 1) / s.SCH);
+      hipLaunchKernelGGL(k_stitch<C>, dim3(div_up(nout / 2, 256)), dim3(256), 0, st, ckeys, cvals, ccount,
+                         (uint32_t)nb, s.SCH, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
+      ZK_CHECK(hipGetLastError());
+      if (final_level) break;
+      // most levels past the first are empty for well-spread scalars: check and stop
+      uint32_t *hc = reinterpret_cast<uint32_t *>(dev.host_staging(4));
+      ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
+      ZK_CHECK(hipStreamSynchronize(st));
+      if (*hc <= (uint32_t)s.SCH) break;  // this level's stitch had one chunk: all complete
+      inK = outK; inV = outV; inCount = nullptr; slots = nout;
+      uint32_t *tk = outK, *tv = outV;
+      outK = altK; outV = altV; altK = tk; altV = tv;
+    }
+  }
+  prof.mark("stitch");
+  {
+    const size_t lanes = (size_t)s.W * s.ylanes;
+    hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
+                       s.r1, s.ylanes, Y);
+    ZK_CHECK(hipGetLastError());
+    prof.mark("ysum");
+  }
+  const int ngrp = s.W * s.J;
+  {
+    const size_t lanes = (size_t)s.W * s.jlanes;
+    hipLaunchKernelGGL(k_jobsum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, s.jlanes, P0);
+    ZK_CHECK(hipGetLastError());
+    prof.mark("jobsum");
+  }
+  uint32_t *src = P0;
+  hipLaunchKernelGGL(k_export<C>, dim3(div_up(ngrp, 64)), dim3(64), 0, st, src, ngrp, exp);
+  ZK_CHECK(hipGetLastError());
+  const size_t expbytes = (size_t)ngrp * 4 * C::NP64 * 8;
+  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(expbytes));
+  ZK_CHECK(hipMemcpyAsync(h, exp, expbytes, hipMemcpyDeviceToHost, st));
+  ZK_CHECK(hipStreamSynchronize(st));
+  if (kt.enabled) {
+    float ms = 0;
+    ZK_CHECK(hipEventElapsedTime(&ms, kt.ev0, kt.ev1));
+    kt.total_ms += ms;
+    kt.launches++;
+  }
+  prof.mark("export");
+  const auto t0 = std::chrono::steady_clock::now();
+  finish_host<C>(s, h, out);
+  prof.report(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+}
+
+// host: combine the per-(window, job) sums (XYZZ, canonical reference form; job order
+// of k_jobsum: total, U_{0,0..l0-1}, U_{1,0..l1-1}):
+//   window w: sum_m (m+1) B_m = sum_b 2^b U_{0,b} + 2^l0 sum_b 2^b U_{1,b} + Total
+//   result  = sum_w 2^(c w) (window sum)
+// Every term is 2^e * Z with e = c w + b, c w + l0 + b or c w (< c (w+1)), so one
+// Horner pass over e (c W - 1 doublings) does it all; on one host core a point op
+// costs ~0.4 us against ~20 us for a lone GPU lane, which is why this serial tail
+// stays here.
+template <class C>
+static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<typename HostOf<C>::Fp> &out) {
+  using HF = typename HostOf<C>::Fp;
+  const int NP = C::NP64;
+  const int emax = s.c * s.W - 1;
+  std::vector<zkh::Xyzz<HF>> Z(emax + 1);
+  for (auto &z : Z) zkh::xyzz_set_inf(z);
+  for (int w = 0; w < s.W; w++) {
+    for (int j = 0; j < s.J; j++) {
+      const uint64_t *q = exported + ((size_t)w * s.J + j) * 4 * NP;
+      zkh::Xyzz<HF> p;
+      memcpy(p.X.v, q + 0 * NP, NP * 8);
+      memcpy(p.Y.v, q + 1 * NP, NP * 8);
+      memcpy(p.ZZ.v, q + 2 * NP, NP * 8);
+      memcpy(p.ZZZ.v, q + 3 * NP, NP * 8);
+      if (zkh::xyzz_is_inf(p)) continue;
+      const int e = s.c * w + (j == 0 ? 0 : j - 1);  // job order of k_jobsum
+      zkh::xyzz_add(Z[e], Z[e], p);
+    }
+  }
+  zkh::Xyzz<HF> acc;
+  zkh::xyzz_set_inf(acc);
+  for (int e = emax; e >= 0; e--) {
+    zkh::xyzz_dbl(acc, acc);
+    zkh::xyzz_add(acc, acc, Z[e]);
+  }
+  zkh::xyzz_to_proj(out, acc);
+}
+
+// ---------------------------------------------------------------------------
+// public (C++) entry points used by the C ABI layer
+
+template <class C>
+void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs, bool mont,
+            int window, uint64_t *out_proj) {
+  using HF = typename HostOf<C>::Fp;
+  Device &dev = current_device();
+  std::lock_guard<std::mutex> lock(dev.mu);
+  zkh::Proj<HF> r;
+  msm_run<C>(dev, n, scalars, nl, points, host_inputs, mont, window, r);
+  memcpy(out_proj + 0 * C::NP64, r.X.v, C::NP64 * 8);
+  memcpy(out_proj + 1 * C::NP64, r.Y.v, C::NP64 * 8);
+  memcpy(out_proj + 2 * C::NP64, r.Z.v, C::NP64 * 8);
+}
+
+}  // namespace zk

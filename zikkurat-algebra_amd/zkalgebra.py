@@ -50,14 +50,15 @@ ARR_OPS = ["is_valid", "is_zero", "is_one", "is_equal", "set_zero", "set_one", "
 REFERENCE_SYMBOLS += [f"{c}_arr_mont_{o}" for c in CURVES for o in ARR_OPS] + [
     f"{c}_poly_mont_{k}_by_vanishing" for c in CURVES for k in ("div", "quot")] + [
     f"{c}_G1_proj_{f}" for c in CURVES for f in ("batch_from_affine", "batch_to_affine", "fft_forward",
-                                                  "fft_inverse")]
+                                                  "fft_inverse")] + [
+    f"{c}_G2_proj_MSM_{k}_coeff_{o}_out" for c in CURVES for k in ("mont", "std") for o in ("proj", "affine")]
 EXTENSION_SYMBOLS = [
     "zkg_version", "zkg_device_count", "zkg_set_device", "zkg_device_malloc", "zkg_device_free",
     "zkg_memcpy_htod", "zkg_memcpy_dtoh", "zkg_device_synchronize", "zkg_g1_msm_device", "zkg_ntt_device",
     "zkg_g1_proj_add", "zkg_g1_proj_normalize", "zkg_g1_proj_to_affine", "zkg_gen_fr", "zkg_gen_g1_points",
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
     "zkg_field_mul_rate", "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
-    "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device",
+    "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
 ]
 
 _lib = None
@@ -205,6 +206,19 @@ def msm_proj(curve, coeffs, proj_points):
     aff = np.stack([g1_to_affine(curve, p) for p in proj_points]) if len(proj_points) else \
         np.zeros((0, 2 * NLIMBS_P[curve]), dtype=np.uint64)
     return msm(curve, coeffs, np.ascontiguousarray(aff))
+
+
+def g2_msm(curve, coeffs, points, std=False, affine=False):
+    """G2 MSM (<C>_G2_proj_MSM_*_coeff_*_out): points are affine G2 (x0 x1 y0 y1, Montgomery Fp)"""
+    if coeffs.ndim != 2 or points.ndim != 2 or coeffs.shape[0] != points.shape[0]:
+        raise ValueError("msm: incompatible array dimensions")
+    if points.shape[1] != 4 * NLIMBS_P[curve]:
+        raise ValueError("msm: G2 points must be affine (x, y) over Fp2 in Montgomery form")
+    require_gpu()
+    out = np.zeros((4 if affine else 6) * NLIMBS_P[curve], dtype=np.uint64)
+    name = f"{curve}_G2_proj_MSM_{'std' if std else 'mont'}_coeff_{'affine' if affine else 'proj'}_out"
+    getattr(load(), name)(coeffs.shape[0], _p(coeffs), _p(points), _p(out), coeffs.shape[1])
+    return out
 
 
 def g1_to_affine(curve, proj):

@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Measurement of the SURVEY.md 8f rows (GPU box): Fr vector ops, division by a
+vanishing polynomial, G1 batch_to_affine, G1 group FFT, G2 MSM.
+
+Every GPU figure is device-resident (inputs already in HBM, hipDeviceSynchronize around
+the timed loop); HBM rooflines use ALGORITHMIC bytes (operands read once + result written
+once).  The reference's own C (oracle/_ref, 1 host core) is timed on a bounded sample of
+the same workload for scale.  Prints one JSON object.
+
+    python tools/bench_ext.py [--quick]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import zkalgebra as zk  # noqa: E402
+from oracle.oracle import Reference  # noqa: E402
+
+HBM = 8000.0  # GB/s, MI355X_MICROARCH.md
+CURVE = "bls12_381"
+
+
+def timeit(fn, reps):
+    fn()
+    zk.load().zkg_device_synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    zk.load().zkg_device_synchronize()
+    return (time.perf_counter() - t) / reps
+
+
+def cpu_time(fn):
+    t = time.perf_counter()
+    fn()
+    return time.perf_counter() - t
+
+
+def hbm(bytes_, sec):
+    gbs = bytes_ / sec / 1e9
+    return {"bound": "hbm", "achieved": gbs, "peak": HBM, "unit": "GB/s", "frac": gbs / HBM}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    args = ap.parse_args()
+    zk.require_gpu()
+    ref = Reference() if Reference.available() else None
+    out = {"curve": CURVE, "data": "synthetic (zk_gen.cpp generator; G2 points from the reference's generator)"}
+    lib = zk.load()
+    P = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+    # ---------------------------------------------------------------- Fr vector ops, 2^24
+    m = 22 if args.quick else 24
+    n = 1 << m
+    a, b = zk.gen_fr(CURVE, 1, n), zk.gen_fr(CURVE, 2, n)
+    da, db, dt = zk.DeviceBuffer(a), zk.DeviceBuffer(b), zk.DeviceBuffer.empty(a.nbytes)
+    k = zk.gen_fr(CURVE, 3, 1)[0]
+    arr = {}
+    for op, nread, kw in (("add", 2, {}), ("mul", 2, {}), ("scale", 1, {"kA": k}), ("Ax_plus_y", 2, {"kA": k}),
+                          ("inv", 1, {}), ("div", 2, {})):
+        sec = timeit(lambda: zk.arr_op_device(CURVE, op, n, da, db if nread == 2 else None, None,
+                                              d_tgt=dt, **kw), 5)
+        arr[op] = {"n": n, "ms": sec * 1e3, "elems_per_s": n / sec, "roofline": hbm((nread + 1) * 32 * n, sec)}
+    sec = timeit(lambda: lib.zkg_arr_powers_device(1, n, P(k), P(k), dt.ptr), 5)
+    arr["powers"] = {"n": n, "ms": sec * 1e3, "elems_per_s": n / sec, "roofline": hbm(32 * n, sec)}
+    res = np.zeros(4, np.uint64)
+    sec = timeit(lambda: lib.zkg_arr_dot_device(1, n, da.ptr, db.ptr, P(res)), 5)
+    arr["dot_prod"] = {"n": n, "ms": sec * 1e3, "elems_per_s": n / sec, "roofline": hbm(64 * n, sec)}
+    if ref:
+        s = 1 << 20
+        w = np.zeros((s, 4), np.uint64)
+        for op in ("mul", "inv"):
+            args_ = (a[:s], b[:s]) if op == "mul" else (a[:s],)
+            t = cpu_time(lambda: ref.arr(CURVE, "arr_mont_" + op, s, *args_, w))
+            arr[op]["cpu_reference"] = {"elems_per_s": s / t, "cores": 1, "sample": f"2^20 elements, {op}"}
+    out["fr_vector_ops"] = arr
+
+    # ---------------------------------------------------------------- div_by_vanishing (PLONK-like)
+    nv = 1 << (20 if args.quick else 22)
+    poly = zk.gen_fr(CURVE, 4, 3 * nv)
+    dp = zk.DeviceBuffer(poly)
+    dq = zk.DeviceBuffer.empty(2 * nv * 32)
+    dr = zk.DeviceBuffer.empty(nv * 32)
+    eta = zk.gen_fr(CURVE, 5, 1)[0]
+    lib.zkg_poly_div_by_vanishing_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                                     ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_void_p,
+                                                     ctypes.c_int, ctypes.c_void_p]
+    sec = timeit(lambda: lib.zkg_poly_div_by_vanishing_device(1, 3 * nv, dp.ptr, nv, P(eta), 2 * nv, dq.ptr, nv,
+                                                              dr.ptr), 5)
+    out["div_by_vanishing"] = {"deg": 3 * nv - 1, "n": nv, "ms": sec * 1e3,
+                               "coeffs_per_s": 3 * nv / sec, "roofline": hbm((3 * nv + 3 * nv) * 32, sec)}
+    for d in (dp, dq, dr, da, db, dt):
+        d.free()
+
+    # ---------------------------------------------------------------- G1 batch_to_affine, 2^20
+    np_ = 1 << 20
+    aff = zk.gen_points(CURVE, 6, np_)
+    proj = zk.batch_from_affine(CURVE, aff)
+    dpj, daf = zk.DeviceBuffer(proj), zk.DeviceBuffer.empty(aff.nbytes)
+    lib.zkg_g1_batch_to_affine_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    sec = timeit(lambda: lib.zkg_g1_batch_to_affine_device(1, np_, dpj.ptr, daf.ptr), 5)
+    out["g1_batch_to_affine"] = {"n": np_, "ms": sec * 1e3, "points_per_s": np_ / sec,
+                                 "roofline": hbm((144 + 96) * np_, sec)}
+    if ref:
+        s = 1 << 14
+        w = np.zeros((s, 12), np.uint64)
+        t = cpu_time(lambda: ref.arr(CURVE, "G1_proj_batch_to_affine", s, proj[:s], w))
+        out["g1_batch_to_affine"]["cpu_reference"] = {"points_per_s": s / t, "cores": 1, "sample": "2^14 points"}
+    dpj.free()
+    daf.free()
+
+    # ---------------------------------------------------------------- G1 group FFT
+    fm = 12 if args.quick else 16
+    N = 1 << fm
+    proj = zk.batch_from_affine(CURVE, zk.gen_points(CURVE, 7, N))
+    sg = zk.get_fft_subgroup(CURVE, fm)
+    ds, dd = zk.DeviceBuffer(proj), zk.DeviceBuffer.empty(proj.nbytes)
+    lib.zkg_g1_fft_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.c_void_p, ctypes.c_void_p]
+    g = sg.gen_array()
+    fft = {}
+    for name, inv, smuls in (("forward", 0, N // 2 * fm), ("inverse", 1, N * fm)):
+        sec = timeit(lambda: lib.zkg_g1_fft_device(1, inv, fm, P(g), ds.ptr, dd.ptr), 1)
+        fft[name] = {"log_n": fm, "ms": sec * 1e3, "points_per_s": N / sec, "scalar_muls": smuls,
+                     "scalar_muls_per_s": smuls / sec}
+    if ref:
+        cm = 8
+        sg8 = zk.get_fft_subgroup(CURVE, cm)
+        small = proj[:1 << cm].copy()
+        w = np.zeros_like(small)
+        t = cpu_time(lambda: ref.arr(CURVE, "G1_proj_fft_forward", cm, sg8.gen_array(), small, w))
+        fft["forward"]["cpu_reference"] = {"scalar_muls_per_s": (1 << cm) // 2 * cm / t, "cores": 1,
+                                           "sample": "2^8-point forward FFT"}
+    out["g1_group_fft"] = fft
+    ds.free()
+    dd.free()
+
+    # ---------------------------------------------------------------- G2 MSM
+    from test_gpu_g2 import g2_points
+    gm = 16 if args.quick else 18
+    ng = 1 << gm
+    uniq = g2_points(ref, CURVE, min(ng, 1 << 16)) if ref else None
+    if uniq is not None:
+        pts = np.ascontiguousarray(np.resize(uniq, (ng, uniq.shape[1])))
+        sc = zk.gen_fr(CURVE, 8, ng)
+        dsc, dpt = zk.DeviceBuffer(sc), zk.DeviceBuffer(pts)
+        res = np.zeros(36, np.uint64)
+        lib.zkg_g2_msm_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+        sec = timeit(lambda: lib.zkg_g2_msm_device(1, ng, dsc.ptr, 4, 1, dpt.ptr, P(res), 0), 3)
+        g2 = {"n": ng, "ms": sec * 1e3, "pairs_per_s": ng / sec,
+              "roofline": hbm((32 + 192) * ng, sec), "note": "VALU bound (Fp2 products), like G1"}
+        s = 1 << 12
+        w = np.zeros(24, np.uint64)
+        t = cpu_time(lambda: ref.arr(CURVE, "G2_proj_MSM_mont_coeff_affine_out", s, sc[:s], pts[:s], w, 4))
+        g2["cpu_reference"] = {"pairs_per_s": s / t, "cores": 1, "sample": "first 2^12 pairs"}
+        out["g2_msm"] = g2
+        dsc.free()
+        dpt.free()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -91,3 +91,22 @@ def test_config4_bn128_msm_2_24_vs_reference(gpu):
     pts = gpu.gen_points("bn128", cfg["seed"], n)
     got = gpu.msm_affine("bn128", sc, pts)
     assert [int(x) for x in got] == cfg["affine"]
+
+
+def test_config5_bls12_381_msm_2_26_vs_reference(gpu):
+    """BASELINE config 5 at full size on ONE GPU (the reference's Montgomery entry aborts
+    at 2^26, G1_proj.c:631-632 -- ours must not), then as the 8-GPU job splits it: 8
+    contiguous shards whose projective partials are summed in rank order."""
+    cfg = _baseline("config5_bls12_381_msm_2^26")
+    curve = "bls12_381"
+    n = 1 << cfg["log_n"]
+    sc = gpu.gen_fr(curve, cfg["seed"], n)
+    pts = gpu.gen_points(curve, cfg["seed"], n)
+    got = gpu.msm_affine(curve, sc, pts)
+    assert [int(x) for x in got] == cfg["affine"]
+    step = n // 8
+    acc = None
+    for k in range(8):
+        part = gpu.msm(curve, sc[k * step:(k + 1) * step], pts[k * step:(k + 1) * step])
+        acc = part if acc is None else gpu.g1_add(curve, acc, part)
+    assert [int(x) for x in gpu.g1_to_affine(curve, acc)] == cfg["affine"]

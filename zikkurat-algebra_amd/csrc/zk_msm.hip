@@ -4,17 +4,22 @@
 namespace zk {
 
 int msm_default_window(int n) {
-  // GPU window: more buckets are cheap on a wide device, fewer windows save
-  // accumulation work.  (The reference uses round(log2 n - 3.5), G1_proj.c:600; the
-  // result does not depend on the choice.)
+  // GPU window, from window sweeps on MI355X (profiles/r01_v5_window_sweep_*.txt):
+  // 2^10 -> 9, 2^12 -> 9, 2^14 -> 11, 2^16 -> 13, 2^18..2^24 -> 16, 2^25..2^26 -> 20.
+  // (The reference uses round(log2 n - 3.5), G1_proj.c:600; the result does not depend on
+  // the choice.)  The accumulation's cost falls with c (fewer windows) while the bucket
+  // reduction's rises with it (W * 2^(c-1) buckets): c = 16 balances them from 2^18 to 2^24.
   if (n <= 1) return 4;
-  int lg = ilog2((unsigned)n);
-  int c = lg - 4;
+  const int lg = ilog2((unsigned)n);
+  int c;
+  if (lg <= 11) c = lg - 1;
+  else if (lg <= 17) c = lg - 3;
+  else if (lg <= 24) c = 16;
+  else c = 20;
   if (c < 4) c = 4;
   if (c > 20) c = 20;
   return c;
 }
-
 
 template void msm_g1<BN254>(int, const uint64_t *, int, const uint64_t *, bool, bool, int, uint64_t *);
 template void msm_g1<BLS381>(int, const uint64_t *, int, const uint64_t *, bool, bool, int, uint64_t *);

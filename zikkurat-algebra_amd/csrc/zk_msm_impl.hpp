@@ -489,7 +489,13 @@ static MsmShape make_shape(int n, int c, int bits) {
   s.r1 = SegRegion{1 << s.l0, clampG((1 << s.l1) / s.QY), 1 << s.l1};  // Y0 sums
   s.ylanes = (s.r0.count * s.r0.G + s.r1.count * s.r1.G + 63) & ~63;
   s.J = c;
-  s.CH = 64;   // entries per thread in the level-0 accumulation
+  // entries per thread in the level-0 accumulation: 64 at scale (~2^17+ lanes), fewer for
+  // small inputs so the serial chain per lane stays short (a lone lane's madd ~12 us)
+  {
+    const size_t ent = (size_t)s.W * (size_t)n;
+    size_t ch = ent >> 17;
+    s.CH = ch >= 64 ? 64 : (ch <= 4 ? 4 : (int)ch);
+  }
   s.SCH = 8;   // items per thread in the stitch levels (mostly pairs: keep it wide)
   s.QA = envQA > 0 ? pow2(envQA) : 8;  // items per lane in the weighted job sums
   s.jlanes = 0;

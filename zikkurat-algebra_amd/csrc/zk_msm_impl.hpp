@@ -726,20 +726,20 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
 
 // host: combine the per-(window, job) sums (XYZZ, canonical reference form; job order
 // of k_jobsum: total, U_{0,0..l0-1}, U_{1,0..l1-1}):
-//   window w: sum_m (m+1) B_m = sum_b 2^b U_{0,b} + 2^l0 sum_b 2^b U_{1,b} + Total
-//   result  = sum_w 2^(c w) (window sum)
-// Every term is 2^e * Z with e = c w + b, c w + l0 + b or c w (< c (w+1)), so one
-// Horner pass over e (c W - 1 doublings) does it all; on one host core a point op
-// costs ~0.4 us against ~20 us for a lone GPU lane, which is why this serial tail
-// stays here.
+//   V_w = sum_j 2^(e_j) P_{w,j}, e_j = 0 (total), j - 1 (bit jobs)   [Horner over c - 1 exponents]
+//   result = sum_w 2^(c w) V_w                                        [Horner over the windows]
+// The V_w are independent: they run on the host thread pool; the cross-window chain of
+// c (W - 1) doublings is the only serial part.  On one host core a point op costs ~0.4 us
+// against ~20 us for a lone GPU lane, which is why this tail stays on the host.
 template <class C>
 static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<typename HostOf<C>::Fp> &out) {
   using HF = typename HostOf<C>::Fp;
   const int NP = C::NP64;
-  const int emax = s.c * s.W - 1;
-  std::vector<zkh::Xyzz<HF>> Z(emax + 1);
-  for (auto &z : Z) zkh::xyzz_set_inf(z);
-  for (int w = 0; w < s.W; w++) {
+  const int E = s.c - 1;  // local exponents 0 .. c-2
+  std::vector<zkh::Xyzz<HF>> V(s.W);
+  host_parallel_for(s.W, [&](int w) {
+    std::vector<zkh::Xyzz<HF>> Z(E);
+    for (auto &z : Z) zkh::xyzz_set_inf(z);
     for (int j = 0; j < s.J; j++) {
       const uint64_t *q = exported + ((size_t)w * s.J + j) * 4 * NP;
       zkh::Xyzz<HF> p;
@@ -748,15 +748,22 @@ static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<t
       memcpy(p.ZZ.v, q + 2 * NP, NP * 8);
       memcpy(p.ZZZ.v, q + 3 * NP, NP * 8);
       if (zkh::xyzz_is_inf(p)) continue;
-      const int e = s.c * w + (j == 0 ? 0 : j - 1);  // job order of k_jobsum
+      const int e = j == 0 ? 0 : j - 1;
       zkh::xyzz_add(Z[e], Z[e], p);
     }
-  }
+    zkh::Xyzz<HF> acc;
+    zkh::xyzz_set_inf(acc);
+    for (int e = E - 1; e >= 0; e--) {
+      zkh::xyzz_dbl(acc, acc);
+      zkh::xyzz_add(acc, acc, Z[e]);
+    }
+    V[w] = acc;
+  });
   zkh::Xyzz<HF> acc;
   zkh::xyzz_set_inf(acc);
-  for (int e = emax; e >= 0; e--) {
-    zkh::xyzz_dbl(acc, acc);
-    zkh::xyzz_add(acc, acc, Z[e]);
+  for (int w = s.W - 1; w >= 0; w--) {
+    for (int k = 0; k < s.c; k++) zkh::xyzz_dbl(acc, acc);
+    zkh::xyzz_add(acc, acc, V[w]);
   }
   zkh::xyzz_to_proj(out, acc);
 }

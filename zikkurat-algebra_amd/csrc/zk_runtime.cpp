@@ -1,5 +1,8 @@
 // zk_runtime.cpp -- per-device context: stream, grow-only arena, pinned staging.
 #include "zk_runtime.hpp"
+#include <atomic>
+#include <condition_variable>
+#include <thread>
 
 namespace zk {
 
@@ -48,6 +51,69 @@ Device &current_device() {
     g_devices[id] = d;
   }
   return *g_devices[id];
+}
+
+namespace {
+struct HostPool {
+  std::mutex run_mu;  // one job at a time
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t gen = 0;
+  const std::function<void(int)> *fn = nullptr;
+  int n = 0;
+  std::atomic<int> next{0}, done{0};
+  int workers = 0;
+  HostPool() {
+    unsigned hw = std::thread::hardware_concurrency();
+    workers = hw > 2 ? (int)(hw - 1 < 7 ? hw - 1 : 7) : 0;
+    for (int i = 0; i < workers; i++) std::thread([this] { loop(); }).detach();
+  }
+  void drain() {
+    for (;;) {
+      const int i = next.fetch_add(1);
+      if (i >= n) break;
+      (*fn)(i);
+      done.fetch_add(1);
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return gen != seen; });
+        seen = gen;
+      }
+      drain();
+    }
+  }
+  void run(int count, const std::function<void(int)> &f) {
+    std::lock_guard<std::mutex> g(run_mu);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      fn = &f;
+      n = count;
+      next = 0;
+      done = 0;
+      gen++;
+    }
+    cv.notify_all();
+    drain();
+    while (done.load() < count) std::this_thread::yield();
+    std::lock_guard<std::mutex> lk(mu);
+    n = 0;  // late-waking workers find nothing to do
+  }
+};
+}  // namespace
+
+void host_parallel_for(int n, const std::function<void(int)> &fn) {
+  if (n <= 0) return;
+  static HostPool *pool = new HostPool();  // leaked on purpose: detached workers outlive static teardown
+  if (n == 1 || pool->workers == 0) {
+    for (int i = 0; i < n; i++) fn(i);
+    return;
+  }
+  pool->run(n, fn);
 }
 
 KernelTimer &dominant_timer() {

@@ -10,6 +10,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -74,6 +75,11 @@ struct KernelTimer {
   long launches = 0;
 };
 KernelTimer &dominant_timer();
+
+// Small persistent host thread pool for the serial-on-GPU tails that split into
+// independent pieces (e.g. the MSM's per-window Horner segments).  run() is
+// synchronous; the calling thread works too.  Calls from several threads serialise.
+void host_parallel_for(int n, const std::function<void(int)> &fn);
 
 inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 

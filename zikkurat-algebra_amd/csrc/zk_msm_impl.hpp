@@ -383,6 +383,154 @@ __global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ bucke
   }
 }
 
+// Quad-cooperative XYZZ addition (add-2008-s) for latency-bound phases: the 4 lanes of an
+// aligned quad hold acc and b REPLICATED and split the 14 products by dependency level
+//   L1: U1 = X1 ZZ2, U2 = X2 ZZ1, S1 = Y1 ZZZ2, S2 = Y2 ZZZ1 | ZZ1 ZZ2, ZZZ1 ZZZ2   (2 deep)
+//   L2: PP = P^2, RR = R^2                                                             (1)
+//   L3: PPP = P PP, Q = U1 PP, ZZ3 = (ZZ1 ZZ2) PP                                      (1)
+//   L4: R (Q - X3), S1 PPP, ZZZ3 = (ZZZ1 ZZZ2) PPP                                     (1)
+// with quad broadcasts in between: 5 product latencies instead of 14.  Every lane executes
+// the same instruction stream (operands picked by selects, not branches); the result is
+// replicated again.  Special cases are decided on replicated values, so quads never split.
+template <class F>
+__device__ __forceinline__ void fe_sel4(Fe<F> &r, const Fe<F> &v0, const Fe<F> &v1, const Fe<F> &v2,
+                                        const Fe<F> &v3, int q) {
+  // explicit masks: a ternary chain here is lowered to an indexed private array (scratch)
+  const uint32_t k0 = 0u - (uint32_t)(q == 0), k1 = 0u - (uint32_t)(q == 1);
+  const uint32_t k2 = 0u - (uint32_t)(q == 2), k3 = 0u - (uint32_t)(q == 3);
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = (v0.v[i] & k0) | (v1.v[i] & k1) | (v2.v[i] & k2) | (v3.v[i] & k3);
+}
+// quad broadcast from lane SRC of the quad: DPP quad_perm [SRC,SRC,SRC,SRC] (one VALU move
+// per word, no LDS round trip)
+template <int SRC, class F>
+__device__ __forceinline__ void fe_bcast(Fe<F> &r, const Fe<F> &v) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++)
+    r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v[i], SRC * 0x55, 0xf, 0xf, false);
+}
+template <class F>
+__device__ __forceinline__ void xyzz_add_quad(Xyzz<F> &acc, const Xyzz<F> &b, uint32_t *__restrict__ park) {
+  if (xyzz_is_inf(b)) return;
+  if (xyzz_is_inf(acc)) { acc = b; return; }
+  const int q = (int)(threadIdx.x & 3);
+  xyzz_store(park, acc);  // only the rare doubling branch reads it back
+  Fe<F> x, y, m1, m2;
+  fe_sel4(x, acc.X, b.X, acc.Y, b.Y, q);
+  fe_sel4(y, b.ZZ, acc.ZZ, b.ZZZ, acc.ZZZ, q);
+  fe_mul(m1, x, y);  // q: U1, U2, S1, S2 (kept in the producing lane)
+  fe_sel4(x, acc.ZZ, acc.ZZZ, acc.ZZ, acc.ZZZ, q);
+  fe_sel4(y, b.ZZ, b.ZZZ, b.ZZ, b.ZZZ, q);
+  fe_mul(m2, x, y);  // q0: ZZ1 ZZ2, q1: ZZZ1 ZZZ2
+  Fe<F> P, R;
+  {
+    Fe<F> u, v;
+    fe_bcast<0>(u, m1);
+    fe_bcast<1>(v, m1);
+    fe_sub(P, v, u);  // U2 - U1
+    fe_bcast<2>(u, m1);
+    fe_bcast<3>(v, m1);
+    fe_sub(R, v, u);  // S2 - S1
+  }
+  Fe<F> PP, RR;
+  fe_sel4(x, P, R, P, R, q);
+  fe_sqr(y, x);  // q0: PP, q1: RR
+  fe_bcast<0>(PP, y);
+  fe_bcast<1>(RR, y);
+  if (fe_is_zero(PP)) {  // P == 0 (replicated: the whole quad agrees)
+    if (fe_is_zero(RR)) {
+      Xyzz<F> a0, d;
+      xyzz_load(a0, park);
+      xyzz_dbl(d, a0);
+      acc = d;
+    } else {
+      xyzz_set_inf(acc);
+    }
+    return;
+  }
+  Fe<F> PPP, Q, ZZ3;
+  {
+    Fe<F> u1, zza;
+    fe_bcast<0>(u1, m1);
+    fe_bcast<0>(zza, m2);
+    fe_sel4(x, P, u1, zza, P, q);
+    fe_mul(y, x, PP);  // q0: PPP, q1: Q, q2: ZZ3
+    fe_bcast<0>(PPP, y);
+    fe_bcast<1>(Q, y);
+    fe_bcast<2>(ZZ3, y);
+  }
+  Fe<F> X3, t;
+  fe_sub(t, RR, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(X3, t, Q);  // X3 = RR - PPP - 2Q
+  fe_sub(t, Q, X3);
+  {
+    Fe<F> s1, zzza;
+    fe_bcast<2>(s1, m1);
+    fe_bcast<1>(zzza, m2);
+    fe_sel4(x, R, s1, zzza, R, q);
+    fe_sel4(y, t, PPP, PPP, t, q);
+  }
+  fe_mul(m1, x, y);  // q0: R (Q - X3), q1: S1 PPP, q2: ZZZ3
+  Fe<F> a0, a1;
+  fe_bcast<0>(a0, m1);
+  fe_bcast<1>(a1, m1);
+  fe_sub(acc.Y, a0, a1);
+  fe_bcast<2>(acc.ZZZ, m1);
+  acc.X = X3;
+  acc.ZZ = ZZ3;
+}
+
+// 7'. k_jobsum on quads: one logical lane = 4 physical lanes (xyzz_add_quad), segment folds
+//     across quads; jlanes counts PHYSICAL lanes (4 x logical, multiple of 64), G <= 16.
+template <class C>
+__global__ void __launch_bounds__(256) k_jobsum_quad(const uint32_t *__restrict__ Y, int W, int c, int l0, int QA,
+                                                     int wlanes, uint32_t *__restrict__ out) {
+  using F = typename C::Fp;
+  __shared__ uint32_t park_lds[256 * xyzz_words<F>()];
+  uint32_t *park = park_lds + threadIdx.x * xyzz_words<F>();
+  const int l1 = c - 1 - l0;
+  const int NY = (1 << l0) + (1 << l1);
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int w = g / wlanes, t = (g % wlanes) >> 2;  // logical lane within the window
+  const bool active = w < W;
+  int j = -1, G = 1, lane = 0, off = 0;
+  for (int jj = 0; jj < c; jj++) {
+    const int n = jj == 0 ? (1 << l0) : (jj <= l0 ? (1 << (l0 - 1)) : (1 << (l1 - 1)));
+    int Gj = n / QA;
+    Gj = Gj < 1 ? 1 : (Gj > 16 ? 16 : Gj);
+    if (t >= off && t < off + Gj) { j = jj; G = Gj; lane = t - off; }
+    off += Gj;
+  }
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  if (active && j >= 0) {
+    const int d = (j == 0 || j <= l0) ? 0 : 1;
+    const int b = j == 0 ? -1 : (d == 0 ? j - 1 : j - 1 - l0);
+    const int ld = d ? l1 : l0;
+    const int n = (b < 0) ? (1 << ld) : (1 << (ld - 1));
+    const int per = n / G;
+    const uint32_t *Yd = Y + ((size_t)w * NY + (d ? (1 << l0) : 0)) * xyzz_words<F>();
+    for (int k = 0; k < per; k++) {
+      const int e = lane * per + k;
+      int v = e;
+      if (b >= 0) {
+        const int lowmask = (1 << b) - 1;
+        v = ((e & ~lowmask) << 1) | (1 << b) | (e & lowmask);
+      }
+      Xyzz<F> p;
+      xyzz_load(p, Yd + (size_t)v * xyzz_words<F>());
+      xyzz_add_quad(acc, p, park);
+    }
+  }
+  for (int o = G >> 1; o >= 1; o >>= 1) {
+    Xyzz<F> other = xyzz_shfl_down(acc, 4 * o, 4 * G);
+    xyzz_add_quad(acc, other, park);
+  }
+  if (active && j >= 0 && lane == 0 && (threadIdx.x & 3) == 0)
+    xyzz_store(out + ((size_t)w * c + j) * xyzz_words<F>(), acc);
+}
+
 // 7. weighted sums of the Y's by bits: per window, job (d, b) for b < l_d is
 //    U_{d,b} = sum_{v: bit b of v} Yd_v (2^(l_d - 1) items) and one job is sum_v Y0_v
 //    (2^l0 items); J = l0 + l1 + 1 = c jobs.  Same segment scheme: jobs ordered by
@@ -700,8 +848,21 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   }
   const int ngrp = s.W * s.J;
   {
-    const size_t lanes = (size_t)s.W * s.jlanes;
-    hipLaunchKernelGGL(k_jobsum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, s.jlanes, P0);
+    static const int quad = env_int("ZK_MSM_QUAD", 1);
+    if (quad) {
+      int jl = 0;  // logical lanes per window, G <= 16
+      for (int j = 0; j < c; j++) {
+        const int n = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
+        int g = n / s.QA;
+        jl += g < 1 ? 1 : (g > 16 ? 16 : g);
+      }
+      const int wl = ((jl + 15) & ~15) * 4;
+      const size_t lanes = (size_t)s.W * wl;
+      hipLaunchKernelGGL(k_jobsum_quad<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, wl, P0);
+    } else {
+      const size_t lanes = (size_t)s.W * s.jlanes;
+      hipLaunchKernelGGL(k_jobsum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, s.jlanes, P0);
+    }
     ZK_CHECK(hipGetLastError());
     prof.mark("jobsum");
   }

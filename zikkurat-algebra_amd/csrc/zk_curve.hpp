@@ -150,8 +150,8 @@ __device__ __forceinline__ void xyzz_add_aff(Xyzz<F> &acc, const Aff<F> &a) {
 // squares PP and RR (products are < 2p and normalised, and PP == 0 <=> P == 0 as p is
 // prime), and Y3 = R (Q - X3) - Y1 PPP is one fe_mul2 (shared reduction).
 // Representation invariant of acc between calls: X, Y normalised limbs with values
-// X < 14p, Y < 6p (not < 2p); ZZ, ZZZ < 2p.  xyzz_settle() restores < 2p before the
-// accumulator leaves the kernel.  Bounds (BLS12-381 Fp: 14 x 28-bit limbs, R'/p > 2^11):
+// X < 14p, Y < 6p (not < 2p); ZZ, ZZZ < 2p.  The accumulator is stored in this form:
+// every later consumer takes X and Y only into products (which accept it).  Bounds (BLS12-381 Fp: 14 x 28-bit limbs, R'/p > 2^11):
 //   P = U2 + 16p - X1 < 18p, limbs < 2^29.6;  R = S2 + 8p - Y1 < 10p
 //   PP, RR, PPP, Q < 2p (products of values < 2^11 p)
 //   X3 = RR + 4p - PPP + 8p - 2Q < 14p;  t = Q + 16p - X3 < 18p
@@ -187,14 +187,6 @@ __device__ __forceinline__ void xyzz_add_aff_lazy(Xyzz<F> &acc, const Aff<F> &a)
   acc.X = X3;
   fe_mul(acc.ZZ, acc.ZZ, PP);
   fe_mul(acc.ZZZ, acc.ZZZ, PPP);
-}
-// bring a lazily accumulated X, Y back below 2p (the form every other kernel expects)
-template <class F>
-__device__ __forceinline__ void xyzz_settle(Xyzz<F> &acc) {
-  if (F::N == 14) {
-    fe_reduce(acc.X);
-    fe_reduce(acc.Y);
-  }
 }
 // dispatch: lazy variant for the 381-bit field, exact variant otherwise (the 254-bit
 // fields have only 3 spare bits per limb and R'/p ~ 2^7.4: not enough for these bounds)

@@ -155,18 +155,6 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ offse
   return lo;
 }
 
-template <class F>
-__device__ __forceinline__ void load_signed_point(Aff<F> &a, bool &inf, const uint32_t *__restrict__ points,
-                                                  uint32_t code) {
-  const uint32_t idx = code & 0x7fffffffu;
-  inf = !aff_load(a, points + (size_t)idx * aff_words<F>());
-  if (!inf && (code & 0x80000000u)) {
-    Fe<F> ny;
-    fe_neg(ny, a.y);
-    a.y = ny;
-  }
-}
-
 // 4. level-0 balanced accumulation: thread t owns sorted entries [t*CH, min((t+1)*CH, total)).
 //    Runs of one bucket that lie entirely inside the chunk are written straight to
 //    buckets[b]; a run that crosses the chunk boundary (the chunk's first and/or last run)
@@ -189,12 +177,26 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
     const uint32_t ce = min(total, cs + (uint32_t)CH);
     uint32_t b = bucket_of(offsets, nb, cs);
     uint32_t bbeg = offsets[b], bend = offsets[b + 1];
+    uint32_t bnext = offsets[min(b + 2, nb)];  // end of the next bucket, loaded ahead
     bool first_run = true;
     Xyzz<F> acc;
     xyzz_set_inf(acc);
+    // Flushes store the accumulator LAZILY (X < 14p, Y < 6p for the 381-bit madd): every
+    // consumer (xyzz_add / xyzz_dbl / k_export) takes X and Y only into products, which
+    // accept those values.  A settle here would cost two products per flush, paid by the
+    // whole wavefront whenever any lane flushes (runs average 32 entries at 2^20).
+    // software pipeline: the point gather for entry e+1 and the list index of entry e+2
+    // are in flight while the madd of entry e runs (clamped to the chunk's last entry, so
+    // every load is in bounds and branch-free); infinity test and negation happen at use
+    const uint32_t last = ce - 1;
+    uint32_t c0 = list[cs], c1 = list[min(cs + 1, last)];
+    Aff<F> P;
+    aff_load(P, points + (size_t)(c0 & 0x7fffffffu) * aff_words<F>());
     for (uint32_t e = cs; e < ce; e++) {
+      Aff<F> Pn;
+      aff_load(Pn, points + (size_t)(c1 & 0x7fffffffu) * aff_words<F>());
+      const uint32_t c2 = list[min(e + 2, last)];
       if (e >= bend) {  // run of bucket b ends inside the chunk
-        xyzz_settle(acc);
         if (first_run && bbeg < cs) {
           xyzz_store(ivals + (size_t)(2 * t) * xyzz_words<F>(), acc);
           k0 = b;
@@ -203,15 +205,26 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
         }
         first_run = false;
         xyzz_set_inf(acc);
-        do { b++; bbeg = offsets[b]; bend = offsets[b + 1]; } while (bend <= e);
+        do {  // next non-empty bucket; the next boundary is already in a register
+          b++;
+          bbeg = bend;
+          bend = bnext;
+          bnext = offsets[min(b + 2, nb)];
+        } while (bend <= e);
       }
-      Aff<F> P;
-      bool inf;
-      load_signed_point(P, inf, points, list[e]);
-      if (!inf) xyzz_acc_aff(acc, P);
+      if (P.x.v[0] != 0xffffffffu) {  // affine infinity is skipped
+        if (c0 & 0x80000000u) {
+          Fe<F> ny;
+          fe_neg(ny, P.y);
+          P.y = ny;
+        }
+        xyzz_acc_aff(acc, P);
+      }
+      P = Pn;
+      c0 = c1;
+      c1 = c2;
     }
     // last run: partial if it started before the chunk or continues after it
-    xyzz_settle(acc);
     if (bbeg < cs || bend > ce) {
       const uint32_t slot = first_run ? 2 * t : 2 * t + 1;
       xyzz_store(ivals + (size_t)slot * xyzz_words<F>(), acc);
@@ -643,6 +656,8 @@ static MsmShape make_shape(int n, int c, int bits) {
     const size_t ent = (size_t)s.W * (size_t)n;
     size_t ch = ent >> 17;
     s.CH = ch >= 64 ? 64 : (ch <= 4 ? 4 : (int)ch);
+    static const int envCH = env_int("ZK_MSM_CH", 0);
+    if (envCH > 0) s.CH = envCH;
   }
   s.SCH = 8;   // items per thread in the stitch levels (mostly pairs: keep it wide)
   s.QA = envQA > 0 ? pow2(envQA) : 8;  // items per lane in the weighted job sums

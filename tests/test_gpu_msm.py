@@ -57,6 +57,20 @@ def test_skewed_buckets(gpu, oracle, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_skewed_large_vs_reference(gpu, reference, curve):
+    """2^16 pairs drawn from 3 scalars plus zeros: a few buckets per window hold ~n/3
+    points each, so the partial-run stitching runs several levels at full chunk size;
+    checked against the reference's own C"""
+    n = 1 << 16
+    rng = np.random.default_rng(77)
+    vals = gpu.gen_fr(curve, 78, 3)
+    sc = vals[rng.integers(0, 3, n)].copy()
+    sc[rng.random(n) < 0.05] = 0
+    pts = gpu.gen_points(curve, 79, n)
+    assert np.array_equal(gpu.msm_affine(curve, sc, pts), reference.msm(curve, sc, pts, mont=True))
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_device_resident_api(gpu, curve):
     n = 5000
     sc = gpu.gen_fr(curve, 41, n)

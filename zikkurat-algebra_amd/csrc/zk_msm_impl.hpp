@@ -246,29 +246,12 @@ static __global__ void __launch_bounds__(256) k_item_flags(const uint32_t *__res
   const uint32_t n = count ? *count : nslots_max;
   flags[i] = (i < n && ikeys[i] < nb) ? 1u : 0u;
 }
-template <class C>
-__global__ void __launch_bounds__(256) k_item_compact(const uint32_t *__restrict__ ikeys, const uint32_t *__restrict__ ivals,
-                                                      const uint32_t *__restrict__ flags, const uint32_t *__restrict__ pos,
-                                                      uint32_t nslots_max, uint32_t *__restrict__ okeys,
-                                                      uint32_t *__restrict__ ovals, uint32_t *__restrict__ ocount) {
-  using F = typename C::Fp;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nslots_max) return;
-  if (i == nslots_max - 1) *ocount = pos[i] + flags[i];
-  if (!flags[i]) return;
-  const uint32_t o = pos[i];
-  okeys[o] = ikeys[i];
-  const uint4 *s = reinterpret_cast<const uint4 *>(ivals + (size_t)i * xyzz_words<F>());
-  uint4 *d = reinterpret_cast<uint4 *>(ovals + (size_t)o * xyzz_words<F>());
-#pragma unroll
-  for (int q = 0; q < xyzz_words<F>() / 4; q++) d[q] = s[q];
-}
-
-// 5b. stitch level: the compacted items (sorted by key) are summed per key with the
-//     same balanced-chunk scheme; complete runs go to buckets[b], runs crossing a chunk
+// 5b. stitch level: the compacted items (sorted by key; payload e at vals[idx[e]]) are
+//     summed per key with the same balanced-chunk scheme; complete runs go to buckets[b], runs crossing a chunk
 //     boundary become the next level's items.  Levels repeat until one chunk remains.
 template <class C>
-__global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+__global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ idx,
+                                                const uint32_t *__restrict__ vals,
                                                 const uint32_t *__restrict__ count, uint32_t nb, int CH,
                                                 uint32_t W, uint32_t B, uint32_t *__restrict__ buckets, uint32_t *__restrict__ okeys,
                                                 uint32_t *__restrict__ ovals, uint32_t nslots) {
@@ -299,7 +282,7 @@ __global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ key
         b = k;
       }
       Xyzz<F> v;
-      xyzz_load(v, vals + (size_t)e * xyzz_words<F>());
+      xyzz_load(v, vals + (size_t)idx[e] * xyzz_words<F>());
       xyzz_add(acc, v);
     }
     const bool cont_out = ce < M && keys[ce] == b;
@@ -313,6 +296,22 @@ __global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ key
   }
   okeys[2 * t] = k0;
   okeys[2 * t + 1] = k1;
+}
+
+// 5a'. index compaction: the valid item slots as (key, slot index) pairs -- the XYZZ
+//      payloads stay where they are and the stitch reads them through the index
+static __global__ void __launch_bounds__(256) k_item_index(const uint32_t *__restrict__ ikeys,
+                                                           const uint32_t *__restrict__ flags,
+                                                           const uint32_t *__restrict__ pos, uint32_t nslots,
+                                                           uint32_t *__restrict__ okeys, uint32_t *__restrict__ oidx,
+                                                           uint32_t *__restrict__ ocount) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots) return;
+  if (i == nslots - 1) *ocount = pos[i] + flags[i];
+  if (!flags[i]) return;
+  const uint32_t o = pos[i];
+  okeys[o] = ikeys[i];
+  oidx[o] = i;
 }
 
 // In-wavefront segmented point sum: the G lanes of an aligned segment (G a power of two
@@ -393,6 +392,79 @@ __global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ bucke
   if (active && lane == 0 && len > 0) {
     const int y = hiY ? (1 << l0) + seg : seg;
     xyzz_store(Y + ((size_t)w * NY + y) * xyzz_words<F>(), acc);
+  }
+}
+
+// 6'. k_ysum2: block-level form of k_ysum, used when each region fills whole 256-lane
+//     blocks (every shape from c = 12 up at the default QY).  Segment s of a block owns the
+//     STRIDED lanes {s, s + S, s + 2S, ...} (S = 256 / G segments per block), so the fold
+//     pairs lane t with lane t + h (h = 128 ... S): the upper half parks its partial in LDS
+//     and drops out, the lower half adds it -- whole wavefronts leave the fold as h
+//     shrinks, where k_ysum's in-wavefront fold keeps every lane adding at every step.
+//     The next bucket's emptiness test (and, with PF, its data) is loaded one iteration
+//     ahead: at one or two waves per SIMD nothing else hides those latencies.
+template <class C, bool PF>
+__global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buckets,
+                                               const uint32_t *__restrict__ offsets, int W, int c, int l0,
+                                               SegRegion r0, SegRegion r1, uint32_t *__restrict__ Y) {
+  using F = typename C::Fp;
+  constexpr int XW = xyzz_words<F>();
+  __shared__ uint4 park4[128 * XW / 4];
+  uint32_t *park = reinterpret_cast<uint32_t *>(park4);
+  const int l1 = c - 1 - l0;
+  const int NY = (1 << l0) + (1 << l1);
+  const int nb0 = r0.count * r0.G / 256, nb1 = r1.count * r1.G / 256;  // blocks per window and region
+  const int w = blockIdx.x / (nb0 + nb1);
+  int rb = blockIdx.x % (nb0 + nb1);
+  const bool hiY = rb < nb0;  // Y1 (region 0) or Y0 (region 1)
+  const SegRegion r = hiY ? r0 : r1;
+  if (!hiY) rb -= nb0;
+  const int G = r.G, S = 256 / G;
+  const int t = threadIdx.x;
+  const int seg = rb * S + t % S, part = t / S;
+  const int per = r.len / G;
+  const uint32_t B = 1u << (c - 1);
+  const uint32_t *wb = buckets + (size_t)w * B * XW;
+  auto bucket_m = [&](int s) -> uint32_t {
+    return hiY ? ((uint32_t)seg << l0) + (uint32_t)s : ((uint32_t)s << l0) + (uint32_t)seg;
+  };
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  uint32_t m = bucket_m(part * per);
+  uint32_t rank = m * (uint32_t)W + (uint32_t)w;
+  uint32_t o0 = offsets[rank], o1 = offsets[rank + 1];
+  Xyzz<F> nxt;
+  if (PF) xyzz_load(nxt, wb + (size_t)m * XW);
+  for (int k = 0; k < per; k++) {
+    const bool full = o1 > o0;  // empty buckets hold garbage (never written)
+    const uint32_t mc = m;
+    Xyzz<F> cur;
+    if (PF) cur = nxt;
+    if (k + 1 < per) {
+      m = bucket_m(part * per + k + 1);
+      rank = m * (uint32_t)W + (uint32_t)w;
+      o0 = offsets[rank];
+      o1 = offsets[rank + 1];
+      if (PF) xyzz_load(nxt, wb + (size_t)m * XW);
+    }
+    if (full) {
+      if (!PF) xyzz_load(cur, wb + (size_t)mc * XW);
+      xyzz_add(acc, cur);
+    }
+  }
+  for (int h = 128; h >= S; h >>= 1) {
+    if (t >= h && t < 2 * h) xyzz_store(park + (size_t)(t - h) * XW, acc);
+    __syncthreads();
+    if (t < h) {
+      Xyzz<F> o;
+      xyzz_load(o, park + (size_t)t * XW);
+      xyzz_add(acc, o);
+    }
+    __syncthreads();
+  }
+  if (t < S) {
+    const int y = hiY ? (1 << l0) + seg : seg;
+    xyzz_store(Y + ((size_t)w * NY + y) * XW, acc);
   }
 }
 
@@ -659,7 +731,8 @@ static MsmShape make_shape(int n, int c, int bits) {
     static const int envCH = env_int("ZK_MSM_CH", 0);
     if (envCH > 0) s.CH = envCH;
   }
-  s.SCH = 8;   // items per thread in the stitch levels (mostly pairs: keep it wide)
+  static const int envSCH = env_int("ZK_MSM_SCH", 0);
+  s.SCH = envSCH >= 2 ? envSCH : 4;  // items per k_stitch thread (swept on MI355X: 4 < 8 < 16)
   s.QA = envQA > 0 ? pow2(envQA) : 8;  // items per lane in the weighted job sums
   s.jlanes = 0;
   for (int j = 0; j < c; j++) {  // same job order / sizes as k_jobsum
@@ -691,7 +764,7 @@ static size_t workspace_bytes(const MsmShape &s) {
   add((size_t)s.n * aff_words<F>() * 4);  // internal-form points
   add(maxent * 4 * 4);                    // keys, vals, sorted keys, sorted vals
   add((nb + 1) * 4);                      // offsets
-  add(ns0 * (xw + 4) * 2 + ns0 * 8 + 64); // level-0 items, compacted items, flags, pos, count
+  add(ns0 * (xw + 4) + ns0 * 16 + 64);    // level-0 items, compacted keys + index, flags, pos, count
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
   add((size_t)s.W * s.NY * xw);              // Y
@@ -779,7 +852,7 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   uint32_t *ikeys0 = dev.arena.take<uint32_t>(ns0);
   uint32_t *ivals0 = dev.arena.take<uint32_t>(ns0 * xw);
   uint32_t *ckeys = dev.arena.take<uint32_t>(ns0);
-  uint32_t *cvals = dev.arena.take<uint32_t>(ns0 * xw);
+  uint32_t *cidx = dev.arena.take<uint32_t>(ns0);
   uint32_t *flags = dev.arena.take<uint32_t>(ns0);
   uint32_t *pos = dev.arena.take<uint32_t>(ns0);
   uint32_t *ccount = dev.arena.take<uint32_t>(16);
@@ -834,12 +907,12 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
       ZK_CHECK(hipGetLastError());
       size_t cb = cub;
       ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, flags, pos, (int)slots, st));
-      hipLaunchKernelGGL(k_item_compact<C>, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, inV, flags, pos,
-                         (uint32_t)slots, ckeys, cvals, ccount);
-      ZK_CHECK(hipGetLastError());
       const bool final_level = slots <= (size_t)s.SCH;  // all items fit one chunk: everything completes
       const size_t nout = final_level ? 2 : 2 * ((slots + s.SCH - 1) / s.SCH);
-      hipLaunchKernelGGL(k_stitch<C>, dim3(div_up(nout / 2, 256)), dim3(256), 0, st, ckeys, cvals, ccount,
+      hipLaunchKernelGGL(k_item_index, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, flags, pos,
+                         (uint32_t)slots, ckeys, cidx, ccount);
+      ZK_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(k_stitch<C>, dim3(div_up(nout / 2, 256)), dim3(256), 0, st, ckeys, cidx, inV, ccount,
                          (uint32_t)nb, s.SCH, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
       ZK_CHECK(hipGetLastError());
       if (final_level) break;
@@ -855,9 +928,21 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   }
   prof.mark("stitch");
   {
-    const size_t lanes = (size_t)s.W * s.ylanes;
-    hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
-                       s.r1, s.ylanes, Y);
+    static const int ys = env_int("ZK_MSM_YSUM", 2);  // 0: k_ysum, 1: k_ysum2, 2: k_ysum2 + data prefetch
+    const int n0 = s.r0.count * s.r0.G, n1 = s.r1.count * s.r1.G;
+    if (ys && n0 % 256 == 0 && n1 % 256 == 0) {
+      const unsigned nblk = (unsigned)(s.W * (n0 + n1) / 256);
+      if (ys == 2)
+        hipLaunchKernelGGL((k_ysum2<C, true>), dim3(nblk), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
+                           s.r1, Y);
+      else
+        hipLaunchKernelGGL((k_ysum2<C, false>), dim3(nblk), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
+                           s.r1, Y);
+    } else {
+      const size_t lanes = (size_t)s.W * s.ylanes;
+      hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0,
+                         s.r0, s.r1, s.ylanes, Y);
+    }
     ZK_CHECK(hipGetLastError());
     prof.mark("ysum");
   }

@@ -145,6 +145,21 @@ static __global__ void __launch_bounds__(256) k_offsets(const uint32_t *__restri
   offsets[b] = lo;
 }
 
+// same offsets from one coalesced pass over the sorted keys: ranks are non-decreasing, so
+// entry e writes offsets[r] = e for every rank r in (rank(e-1), rank(e)] (clamped to nb;
+// zero digits rank >= nb), and the last entry fills the ranks after it with M
+static __global__ void __launch_bounds__(256) k_offsets_scan(const uint32_t *__restrict__ skeys, uint32_t M,
+                                                             uint32_t nb, int c, uint32_t W,
+                                                             uint32_t *__restrict__ offsets) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= M) return;
+  const uint32_t r = min(key_rank(skeys[e], c, W), nb);
+  const uint32_t lo = e ? min(key_rank(skeys[e - 1], c, W), nb) + 1 : 0;
+  for (uint32_t q = lo; q <= r; q++) offsets[q] = e;
+  if (e == M - 1)
+    for (uint32_t q = r + 1; q <= nb; q++) offsets[q] = M;
+}
+
 // first bucket index b with offsets[b+1] > e  (offsets has nb+1 entries)
 __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ offsets, uint32_t nb, uint32_t e) {
   uint32_t lo = 0, hi = nb;  // answer in [lo, hi)
@@ -246,6 +261,73 @@ static __global__ void __launch_bounds__(256) k_item_flags(const uint32_t *__res
   const uint32_t n = count ? *count : nslots_max;
   flags[i] = (i < n && ikeys[i] < nb) ? 1u : 0u;
 }
+// 5c. block stitch level: BS consecutive compacted items (sorted by key; payload e at
+//     vals[idx[e]]) per workgroup, one per lane, summed per key by a segmented
+//     Hillis-Steele scan through LDS (step d: lane t adds lane t-d when both hold the same
+//     key); steps stop as soon as no lane of the block needs one, so short runs (the
+//     common tail-of-one-chunk + head-of-the-next pairs) cost one step and a run of any
+//     length shrinks BS-fold per level.  The last lane of each segment owns its sum: a
+//     whole run goes to its bucket, a run cut by the block edge becomes an item of the
+//     next level in slot 2 blk (the block's first segment, when its run started earlier
+//     -- or when it is also the last one) or 2 blk + 1 (the last segment, when its run
+//     continues), the same layout as k_stitch with SCH = BS.
+template <class C, int BS>
+__global__ void __launch_bounds__(BS) k_stitch_blk(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ idx,
+                                                   const uint32_t *__restrict__ vals,
+                                                   const uint32_t *__restrict__ count, uint32_t nb, uint32_t W,
+                                                   uint32_t B, uint32_t *__restrict__ buckets,
+                                                   uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,
+                                                   uint32_t nout) {
+  using F = typename C::Fp;
+  constexpr int XW = xyzz_words<F>();
+  __shared__ uint4 stitch_lds4[BS * XW / 4];  // [BS][XW] partial sums (<= 64 KB: BS is 128 for G2)
+  uint32_t *lv = reinterpret_cast<uint32_t *>(stitch_lds4);
+  __shared__ uint32_t skey[BS];
+  const uint32_t M = *count;
+  const uint32_t t = threadIdx.x, blk = blockIdx.x;
+  const uint32_t base = blk * BS;
+  if (base >= M) {  // no items: clear this block's output slots
+    if (t < 2 && 2 * blk + t < nout) okeys[2 * blk + t] = nb;
+    return;
+  }
+  const uint32_t nv = min((uint32_t)BS, M - base);  // valid lanes
+  const uint32_t j = base + t;
+  const bool valid = t < nv;
+  const uint32_t key = valid ? keys[j] : 0xffffffffu;
+  skey[t] = key;
+  Xyzz<F> acc;
+  if (valid) xyzz_load(acc, vals + (size_t)idx[j] * XW);
+  else xyzz_set_inf(acc);
+  __syncthreads();
+  for (uint32_t d = 1; d < nv; d <<= 1) {
+    const bool need = valid && t >= d && skey[t - d] == key;
+    if (!__syncthreads_or(need)) break;
+    xyzz_store(lv + (size_t)t * XW, acc);
+    __syncthreads();
+    if (need) {
+      Xyzz<F> o;
+      xyzz_load(o, lv + (size_t)(t - d) * XW);
+      xyzz_add(acc, o);
+    }
+    __syncthreads();
+  }
+  if (!valid) return;
+  const bool seg_last = t == nv - 1 || skey[t + 1] != key;
+  if (!seg_last) return;
+  const bool touches_start = skey[0] == key;
+  const bool touches_end = t == nv - 1;
+  const bool cont_in = touches_start && base > 0 && keys[base - 1] == key;
+  const bool cont_out = touches_end && base + nv < M && keys[base + nv] == key;
+  if (!cont_in && !cont_out) {
+    xyzz_store(buckets + (size_t)bucket_slot(key, W, B) * XW, acc);
+  } else {
+    xyzz_store(ovals + (size_t)(touches_start ? 2 * blk : 2 * blk + 1) * XW, acc);
+  }
+  const uint32_t item_key = (cont_in || cont_out) ? key : nb;
+  if (touches_start) okeys[2 * blk] = item_key;
+  if (touches_end) okeys[2 * blk + 1] = touches_start ? nb : item_key;
+}
+
 // 5b. stitch level: the compacted items (sorted by key; payload e at vals[idx[e]]) are
 //     summed per key with the same balanced-chunk scheme; complete runs go to buckets[b], runs crossing a chunk
 //     boundary become the next level's items.  Levels repeat until one chunk remains.
@@ -716,7 +798,14 @@ static MsmShape make_shape(int n, int c, int bits) {
   s.l1 = c - 1 - s.l0;
   s.NY = (1 << s.l0) + (1 << s.l1);
   auto pow2 = [](int v) { int r = 1; while (2 * r <= v) r *= 2; return r; };  // segments need powers of 2
-  s.QY = envQY > 0 ? pow2(envQY) : 16;  // buckets per lane in the Y sums (swept on MI355X)
+  // buckets per lane in the Y sums: 16 at scale (swept on MI355X), fewer when there are few
+  // buckets, so the sums keep ~64K lanes (2 W B bucket adds) instead of a long serial chain
+  {
+    const size_t adds = 2 * (size_t)s.W * (size_t)s.B;
+    int q = (int)(adds >> 16);
+    q = q < 1 ? 1 : (q > 16 ? 16 : q);
+    s.QY = envQY > 0 ? pow2(envQY) : pow2(q);
+  }
   auto clampG = [](int g) { return g < 1 ? 1 : (g > 64 ? 64 : g); };
   s.r0 = SegRegion{1 << s.l1, clampG((1 << s.l0) / s.QY), 1 << s.l0};  // Y1 sums
   s.r1 = SegRegion{1 << s.l0, clampG((1 << s.l1) / s.QY), 1 << s.l1};  // Y0 sums
@@ -880,8 +969,13 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   prof.mark("digits");
   ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
   prof.mark("sort");
-  hipLaunchKernelGGL(k_offsets, dim3(div_up(nb + 1, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
-                     (uint32_t)nb, c, (uint32_t)s.W, offsets);
+  static const int offs_scan = env_int("ZK_MSM_OFFSCAN", 1);
+  if (offs_scan)
+    hipLaunchKernelGGL(k_offsets_scan, dim3(div_up(maxent, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
+                       (uint32_t)nb, c, (uint32_t)s.W, offsets);
+  else
+    hipLaunchKernelGGL(k_offsets, dim3(div_up(nb + 1, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
+                       (uint32_t)nb, c, (uint32_t)s.W, offsets);
   ZK_CHECK(hipGetLastError());
 
   prof.mark("offsets");
@@ -896,38 +990,45 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   }
   prof.mark("accum");
   // stitch levels: compact the partial items, sum them per bucket, repeat
-  {
-    const uint32_t *inK = ikeys0, *inV = ivals0;
-    const uint32_t *inCount = nullptr;  // level 0: every slot is examined
-    size_t slots = ns0;
-    uint32_t *outK = okA, *outV = ovA, *altK = okB, *altV = ovB;
-    for (;;) {
-      hipLaunchKernelGGL(k_item_flags, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, inCount, (uint32_t)slots,
-                         (uint32_t)nb, flags);
-      ZK_CHECK(hipGetLastError());
-      size_t cb = cub;
-      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, flags, pos, (int)slots, st));
-      const bool final_level = slots <= (size_t)s.SCH;  // all items fit one chunk: everything completes
-      const size_t nout = final_level ? 2 : 2 * ((slots + s.SCH - 1) / s.SCH);
-      hipLaunchKernelGGL(k_item_index, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, flags, pos,
-                         (uint32_t)slots, ckeys, cidx, ccount);
-      ZK_CHECK(hipGetLastError());
+  const uint32_t *inK = ikeys0, *inV = ivals0;
+  size_t slots = ns0;
+  uint32_t *outK = okA, *outV = ovA, *altK = okB, *altV = ovB;
+  // block stitch (k_stitch_blk, BS items per workgroup; 128 for the wide G2 points so the
+  // LDS exchange buffer stays at 64 KB) or the per-thread k_stitch (env ZK_MSM_STITCH_BLK=0)
+  constexpr int STITCH_BS = xyzz_words<F>() > 64 ? 128 : 256;
+  static const int stitch_blk = env_int("ZK_MSM_STITCH_BLK", 1);
+  const size_t stitch_chunk = stitch_blk ? (size_t)STITCH_BS : (size_t)s.SCH;
+  auto stitch_level = [&]() -> bool {  // true: every item completed at this level
+    hipLaunchKernelGGL(k_item_flags, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, (const uint32_t *)nullptr,
+                       (uint32_t)slots, (uint32_t)nb, flags);
+    ZK_CHECK(hipGetLastError());
+    size_t cb = cub;
+    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, flags, pos, (int)slots, st));
+    const size_t chunk = stitch_chunk;
+    const bool final_level = slots <= chunk;  // all items fit one chunk: everything completes
+    const size_t nout = final_level ? 2 : 2 * ((slots + chunk - 1) / chunk);
+    hipLaunchKernelGGL(k_item_index, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, flags, pos, (uint32_t)slots,
+                       ckeys, cidx, ccount);
+    ZK_CHECK(hipGetLastError());
+    if (stitch_blk) {
+      hipLaunchKernelGGL((k_stitch_blk<C, STITCH_BS>), dim3((unsigned)(nout / 2)), dim3(STITCH_BS), 0, st, ckeys, cidx, inV, ccount, (uint32_t)nb, (uint32_t)s.W,
+                         (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
+    } else {
       hipLaunchKernelGGL(k_stitch<C>, dim3(div_up(nout / 2, 256)), dim3(256), 0, st, ckeys, cidx, inV, ccount,
                          (uint32_t)nb, s.SCH, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
-      ZK_CHECK(hipGetLastError());
-      if (final_level) break;
-      // most levels past the first are empty for well-spread scalars: check and stop
-      uint32_t *hc = reinterpret_cast<uint32_t *>(dev.host_staging(4));
-      ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
-      ZK_CHECK(hipStreamSynchronize(st));
-      if (*hc <= (uint32_t)s.SCH) break;  // this level's stitch had one chunk: all complete
-      inK = outK; inV = outV; inCount = nullptr; slots = nout;
-      uint32_t *tk = outK, *tv = outV;
-      outK = altK; outV = altV; altK = tk; altV = tv;
     }
-  }
-  prof.mark("stitch");
-  {
+    ZK_CHECK(hipGetLastError());
+    inK = outK; inV = outV; slots = nout;
+    uint32_t *tk = outK, *tv = outV;
+    outK = altK; outV = altV; altK = tk; altV = tv;
+    return final_level;
+  };
+  // Y sums, job sums, export and the copy back to the host
+  const int ngrp = s.W * s.J;
+  const size_t expbytes = (size_t)ngrp * 4 * C::NP64 * 8;
+  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(expbytes + 64));
+  uint32_t *hc = reinterpret_cast<uint32_t *>(h + ngrp * 4 * C::NP64);  // last stitch level's item count
+  auto reduce_tail = [&]() {
     static const int ys = env_int("ZK_MSM_YSUM", 2);  // 0: k_ysum, 1: k_ysum2, 2: k_ysum2 + data prefetch
     const int n0 = s.r0.count * s.r0.G, n1 = s.r1.count * s.r1.G;
     if (ys && n0 % 256 == 0 && n1 % 256 == 0) {
@@ -945,15 +1046,12 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
     }
     ZK_CHECK(hipGetLastError());
     prof.mark("ysum");
-  }
-  const int ngrp = s.W * s.J;
-  {
     static const int quad = env_int("ZK_MSM_QUAD", 1);
     if (quad) {
       int jl = 0;  // logical lanes per window, G <= 16
       for (int j = 0; j < c; j++) {
-        const int n = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
-        int g = n / s.QA;
+        const int nj = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
+        int g = nj / s.QA;
         jl += g < 1 ? 1 : (g > 16 ? 16 : g);
       }
       const int wl = ((jl + 15) & ~15) * 4;
@@ -965,14 +1063,31 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
     }
     ZK_CHECK(hipGetLastError());
     prof.mark("jobsum");
-  }
-  uint32_t *src = P0;
-  hipLaunchKernelGGL(k_export<C>, dim3(div_up(ngrp, 64)), dim3(64), 0, st, src, ngrp, exp);
-  ZK_CHECK(hipGetLastError());
-  const size_t expbytes = (size_t)ngrp * 4 * C::NP64 * 8;
-  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(expbytes));
-  ZK_CHECK(hipMemcpyAsync(h, exp, expbytes, hipMemcpyDeviceToHost, st));
+    hipLaunchKernelGGL(k_export<C>, dim3(div_up(ngrp, 64)), dim3(64), 0, st, P0, ngrp, exp);
+    ZK_CHECK(hipGetLastError());
+    ZK_CHECK(hipMemcpyAsync(h, exp, expbytes, hipMemcpyDeviceToHost, st));
+  };
+  // Levels 0 and 1 and the whole tail are enqueued without a host round trip: for
+  // well-spread scalars two levels complete every bucket.  Only when level 1 still leaves
+  // more than one chunk of items (skewed scalars) does the host run further levels and
+  // redo the tail.
+  static const int spec = env_int("ZK_MSM_SPEC", 3);  // levels enqueued before the first check
+  bool done = false;
+  for (int lv = 0; lv < spec && !done; lv++) done = stitch_level();
+  prof.mark("stitch");
+  if (!done) ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
+  reduce_tail();
   ZK_CHECK(hipStreamSynchronize(st));
+  if (!done && *hc > (uint32_t)stitch_chunk) {
+    for (;;) {
+      if (stitch_level()) break;
+      ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
+      ZK_CHECK(hipStreamSynchronize(st));
+      if (*hc <= (uint32_t)stitch_chunk) break;  // this level's stitch had one chunk: all complete
+    }
+    reduce_tail();
+    ZK_CHECK(hipStreamSynchronize(st));
+  }
   if (kt.enabled) {
     float ms = 0;
     ZK_CHECK(hipEventElapsedTime(&ms, kt.ev0, kt.ev1));

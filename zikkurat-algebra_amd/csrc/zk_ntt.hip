@@ -29,6 +29,10 @@ namespace zk {
 
 constexpr int NTT_THREADS = 256;
 constexpr int NTT_TILE = 1024;  // elements per workgroup tile for multi-pass transforms
+// Inner twiddles are read from a global (L1/L2-resident, a few KB) internal-limb table with
+// 48-B rows (3 x 16-B loads) rather than staged in LDS: the 1024-element tile alone is
+// 36 KB, so dropping the 4.6 KB twiddle copy lets 4 instead of 3 workgroups share a CU.
+constexpr int ITW_STRIDE = 12;
 
 // ---------------------------------------------------------------------------- tables
 
@@ -96,6 +100,18 @@ __global__ void k_tw_inner(uint64_t *__restrict__ itw, int m, int r, const uint6
   fe_store_ref(itw + (size_t)j * F::N64, w);
 }
 
+// the same table in internal limbs, ITW_STRIDE u32 per entry (exactly what fe_load_ref gives)
+template <class F>
+__global__ void k_tw_inner_int(uint32_t *__restrict__ itw_i, const uint64_t *__restrict__ itw, int n) {
+  static_assert(F::N <= ITW_STRIDE, "inner twiddle rows hold F::N limbs");
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  Fe<F> w;
+  fe_load_ref(w, itw + (size_t)j * F::N64);
+#pragma unroll
+  for (int q = 0; q < ITW_STRIDE; q++) itw_i[(size_t)j * ITW_STRIDE + q] = q < F::N ? w.v[q] : 0u;
+}
+
 // ---------------------------------------------------------------------------- pass kernel
 
 template <class F>
@@ -117,7 +133,7 @@ __device__ __forceinline__ void lds_put(uint32_t *p, const Fe<F> &x) {
 // next stage and the pass's closing product (twiddle / scale / one) bring them back
 // below 2p.  Limb bound: normalised (< 2^29) at round entry, < 2^31.4 at round exit.
 template <class F>
-__device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int r, int G) {
+__device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restrict__ itw, int r, int G) {
   constexpr int NW = F::N;
   const int R = 1 << r;
   const int tid = threadIdx.x;
@@ -125,7 +141,7 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int
   if (r >= 2) {  // first radix-4 round: twiddles w_2^0 = w_4^0 = 1, only w_4^1 is non-trivial
     const int q4 = R >> 2;
     Fe<F> w3;
-    lds_get(w3, itw + (size_t)(R / 4) * NW);  // w_4 = w_R^(R/4)
+    lds_get(w3, itw + (size_t)(R / 4) * ITW_STRIDE);  // w_4 = w_R^(R/4)
     for (int u = tid; u < G * q4; u += NTT_THREADS) {
       const int g = u / q4, j = u % q4;
       const int i0 = g * R + j * 4;
@@ -168,9 +184,9 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int
       lds_get(a1, data + (size_t)(i0 + half) * NW);
       lds_get(a2, data + (size_t)(i0 + 2 * half) * NW);
       lds_get(a3, data + (size_t)(i0 + 3 * half) * NW);
-      lds_get(w1, itw + (size_t)(off * (R / (2 * half))) * NW);           // w_{2h}^off
-      lds_get(w2, itw + (size_t)(off * (R / (4 * half))) * NW);           // w_{4h}^off
-      lds_get(w3, itw + (size_t)((off + half) * (R / (4 * half))) * NW);  // w_{4h}^(off+h)
+      lds_get(w1, itw + (size_t)(off * (R / (2 * half))) * ITW_STRIDE);           // w_{2h}^off
+      lds_get(w2, itw + (size_t)(off * (R / (4 * half))) * ITW_STRIDE);           // w_{4h}^off
+      lds_get(w3, itw + (size_t)((off + half) * (R / (4 * half))) * ITW_STRIDE);  // w_{4h}^(off+h)
       // stage s
       Fe<F> b0, b1, b2, b3;
       fe_mul(t, a1, w1);
@@ -207,7 +223,7 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *itw, int
       Fe<F> a, b, w, t, x, y;
       lds_get(a, data + (size_t)i0 * NW);
       lds_get(b, data + (size_t)(i0 + half) * NW);
-      lds_get(w, itw + (size_t)(off * (R / (2 * half))) * NW);
+      lds_get(w, itw + (size_t)(off * (R / (2 * half))) * ITW_STRIDE);
       fe_mul(t, b, w);
       fe_add_lazy(x, a, t);
       fe_sub_lazy(y, a, t);
@@ -232,7 +248,7 @@ struct PassArgs {
 //                  tile = G instances with consecutive k_0; output to natural index
 template <class F>
 __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__restrict__ src, uint64_t *__restrict__ dst,
-                                                          PassArgs a, const uint64_t *__restrict__ itw_g,
+                                                          PassArgs a, const uint32_t *__restrict__ itw_i,
                                                           const uint64_t *__restrict__ tab,
                                                           const uint64_t *__restrict__ scale) {
   extern __shared__ uint32_t lds[];
@@ -240,15 +256,9 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
   const int r = a.r, G = a.G, S = a.S;
   const int R = 1 << r;
   uint32_t *data = lds;                          // [G][R] elements
-  uint32_t *itw = lds + (size_t)G * R * NW;      // [R/2] inner twiddles
+  const uint32_t *itw = (const uint32_t *)__builtin_assume_aligned(itw_i, 16);  // [R/2] inner twiddles
   const int tid = threadIdx.x;
   const int tile = blockIdx.x;
-
-  for (int j = tid; j < R / 2; j += NTT_THREADS) {
-    Fe<F> w;
-    fe_load_ref(w, itw_g + (size_t)j * F::N64);
-    lds_put(itw + (size_t)j * NW, w);
-  }
 
   // instance geometry of this tile
   size_t hi_base = 0;  // non-last: hi * R * S + lo0
@@ -348,6 +358,7 @@ static void split_digits(int m, std::vector<int> &d) {
 struct TwSet {
   uint64_t *mem = nullptr;       // one allocation
   std::vector<uint64_t *> inner; // per pass: R_p/2 inner twiddles
+  std::vector<uint32_t *> inner_i; // the same, internal limbs, ITW_STRIDE u32 per entry
   std::vector<uint64_t *> tab;   // per non-last pass: R_p * S_p table
   uint64_t *scale = nullptr;     // 1/N (reference form) for the single-pass inverse
   size_t bytes = 0;
@@ -402,6 +413,7 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
   for (int p = 0; p < P; p++) {
     S >>= dig[p];
     words += ((size_t)1 << dig[p]) / 2 * el + el;
+    words += ((size_t)1 << dig[p]) / 2 * (ITW_STRIDE / 2) + 2;
     if (p < P - 1) { tab_words[p] = ((size_t)1 << dig[p]) * S * el; words += tab_words[p]; }
     T <<= dig[p];
   }
@@ -450,6 +462,13 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
       ZK_CHECK(hipGetLastError());
     }
     ts.inner.push_back(inner);
+    uint32_t *inner_i = (uint32_t *)take(((size_t)1 << r) / 2 * (ITW_STRIDE / 2) + 2);
+    if (r > 0) {
+      hipLaunchKernelGGL(k_tw_inner_int<F>, dim3(div_up(((size_t)1 << r) / 2, 256)), dim3(256), 0, st, inner_i, inner,
+                         (1 << r) / 2);
+      ZK_CHECK(hipGetLastError());
+    }
+    ts.inner_i.push_back(inner_i);
     if (p < P - 1) {
       uint64_t *tab = take(tab_words[p]);
       const size_t cnt = ((size_t)1 << r) * S;
@@ -520,7 +539,7 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
       if (G > (1 << dig[0])) G = 1 << dig[0];
     }
     const size_t ntiles = N / ((size_t)R * G);
-    const size_t lds = ((size_t)G * R + R / 2) * F::N * 4;
+    const size_t lds = (size_t)G * R * F::N * 4;
     pa.r = r;
     pa.S = (int)S;
     pa.T = (int)T;
@@ -528,7 +547,7 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     pa.G = G;
     ZK_CHECK(hipFuncSetAttribute((const void *)k_ntt_pass<F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (kt.enabled && p == 0) ZK_CHECK(hipEventRecord(kt.ev0, st));
-    hipLaunchKernelGGL(k_ntt_pass<F>, dim3((unsigned)ntiles), dim3(NTT_THREADS), lds, st, in, out, pa, tw.inner[p],
+    hipLaunchKernelGGL(k_ntt_pass<F>, dim3((unsigned)ntiles), dim3(NTT_THREADS), lds, st, in, out, pa, tw.inner_i[p],
                        tw.tab[p], last ? tw.scale : nullptr);
     ZK_CHECK(hipGetLastError());
     if (kt.enabled && last) ZK_CHECK(hipEventRecord(kt.ev1, st));

@@ -817,6 +817,10 @@ static MsmShape make_shape(int n, int c, int bits) {
     const size_t ent = (size_t)s.W * (size_t)n;
     size_t ch = ent >> 17;
     s.CH = ch >= 64 ? 64 : (ch <= 4 ? 4 : (int)ch);
+    // from 2^25 entries on (BLS12-381 2^21+, BN128 2^21+) 128 per lane still leaves >= 2^18
+    // lanes and halves the partial items the stitch has to sum (MI355X sweep,
+    // profiles/r01_v7_ch_sweep.txt: BLS12-381 2^23 stitch 1.85 -> 0.76 ms, 25.0 -> 23.8 ms)
+    if (ent >= ((size_t)1 << 25)) s.CH = 128;
     static const int envCH = env_int("ZK_MSM_CH", 0);
     if (envCH > 0) s.CH = envCH;
   }

@@ -1,8 +1,47 @@
+#!/bin/bash
+# One parameterised GPU-box job (run through gpurun from the repo root):
+#   gpurun --timeout 900 -- bash tools/gpu_job.sh TAG step [step ...]
+# Steps (each under its own timeout; the job stops at the first failure):
+#   tests     pytest -m gpu                       -> gpurun_out/TAG_tests.log
+#   smoke     __graft_entry__.smoke()             -> gpurun_out/TAG_smoke.log
+#   bench     python bench.py (defaults)          -> gpurun_out/TAG_bench.json
+#   bench2    bench.py as 2 ranks on the one GPU (gloo exchange) -> gpurun_out/TAG_bench2.json
+#   prof      rocprofv3 --kernel-trace --stats of a short bench -> gpurun_out/TAG_prof/
+#   pmcf      rocprofv3 --pmc FETCH_SIZE (own pass) -> gpurun_out/TAG_pmcf/
+#   pmcw      rocprofv3 --pmc WRITE_SIZE (own pass) -> gpurun_out/TAG_pmcw/
+#   ceiling   tools/microbench/valu_ceiling (prebuilt) -> gpurun_out/TAG_ceiling.json
+#   ext       tools/bench_ext.py                  -> gpurun_out/TAG_ext.json
+#   phases    MSM phase profile at several sizes  -> gpurun_out/TAG_phases.txt
+#   cmd       the command in $JOB_CMD             -> gpurun_out/TAG_cmd.log
 set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python -m pytest tests -x -q -m gpu > gpurun_out/gputests8.log 2>&1; echo tests=$?
-timeout -k 10 300 python bench.py > gpurun_out/bench8.json 2> gpurun_out/bench8.err; echo bench=$?
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 3 --warmup 1 --no-ntt > gpurun_out/bench8_dist2.json 2> gpurun_out/bench8_dist2.err; echo dist=$?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --ntt-steps 3 > gpurun_out/bench8p.json 2>gpurun_out/bench8p.err; echo prof=$?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc8a -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --ntt-steps 2 > /dev/null 2>gpurun_out/pmc8a.err; echo pmca=$?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc8b -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --ntt-steps 2 > /dev/null 2>gpurun_out/pmc8b.err; echo pmcb=$?
+TAG=$1
+shift
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+O=gpurun_out/$TAG
+BENCH_SHORT="bench.py --steps 5 --warmup 2 --no-cpu-baseline --ntt-steps 3"
+for step in "$@"; do
+  echo "[$(date +%T)] step $step"
+  case $step in
+    tests) timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > ${O}_tests.log 2>&1 ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 ;;
+    bench) timeout -k 10 400 python -u bench.py > ${O}_bench.json 2> ${O}_bench.err ;;
+    bench2) timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+              --master-port 29517 bench.py --gpus 2 --backend gloo --steps 3 --warmup 1 > ${O}_bench2.json 2> ${O}_bench2.err ;;
+    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d ${O}_prof -o run --output-format csv -- python3 $BENCH_SHORT \
+              > ${O}_prof_bench.json 2> ${O}_prof.err ;;
+    pmcf) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d ${O}_pmcf -o run --output-format csv -- python3 $BENCH_SHORT \
+              > /dev/null 2> ${O}_pmcf.err ;;
+    pmcw) timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d ${O}_pmcw -o run --output-format csv -- python3 $BENCH_SHORT \
+              > /dev/null 2> ${O}_pmcw.err ;;
+    ceiling) timeout -k 10 120 tools/microbench/valu_ceiling > ${O}_ceiling.json 2> ${O}_ceiling.err ;;
+    ext) timeout -k 10 400 python -u tools/bench_ext.py > ${O}_ext.json 2> ${O}_ext.err ;;
+    phases) timeout -k 10 300 python -u tools/sweep_window.py phases > ${O}_phases.txt 2>&1 ;;
+    cmd) timeout -k 10 ${JOB_TIMEOUT:-300} bash -c "$JOB_CMD" > ${O}_cmd.log 2>&1 ;;
+    *) echo "unknown step $step"; false ;;
+  esac
+  rc=$?
+  echo "[$(date +%T)] step $step rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
+echo "job $TAG ok"

@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Instruction counts of a kernel's hot loop, from the compiler's gfx950 assembly.
+
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 --save-temps -c zk_msm.hip   (in a scratch dir)
+    python tools/isa_count.py zk_msm-hip-amdgcn-amd-amdhsa-gfx950.s 'k_accumINS_6BLS381' [--json out]
+
+Splits the function into basic blocks, uses LLVM's loop annotations ("in Loop: Header=...
+Depth=d") to collect the blocks of every loop, and prints per-block and per-loop opcode
+counts.  The VALU roofline in bench.py is priced from these counts: the number of
+v_mad_u64_u32 (and of the other VALU instructions) one loop iteration issues, times the
+measured per-instruction issue ceiling (tools/microbench/valu_ceiling.hip).
+"""
+import argparse
+import collections
+import json
+import re
+import sys
+
+
+def function_body(lines, sym):
+    start = None
+    for i, l in enumerate(lines):
+        if start is None and re.match(r"^_Z\S*%s\S*:" % re.escape(sym), l):
+            start = i
+            name = l.split(":")[0]
+        elif start is not None and l.startswith(".Lfunc_end"):
+            return name, lines[start:i]
+    raise SystemExit(f"symbol matching {sym!r} not found")
+
+
+def blocks_of(body):
+    blocks = []
+    cur = {"label": "entry", "loop": None, "depth": 0, "ops": collections.Counter(), "n": 0}
+    for l in body[1:]:
+        m = re.match(r"^(\.LBB\w+):(.*)$", l)
+        if m:
+            blocks.append(cur)
+            comment = m.group(2)
+            hm = re.search(r"Header=(BB\w+) Depth=(\d+)", comment)
+            if "Loop Header" in comment:
+                dm = re.search(r"Depth=(\d+)", comment)
+                loop, depth = m.group(1)[2:], int(dm.group(1)) if dm else 1
+            elif hm:
+                loop, depth = hm.group(1), int(hm.group(2))
+            else:
+                loop, depth = None, 0
+            cur = {"label": m.group(1), "loop": loop, "depth": depth, "ops": collections.Counter(), "n": 0}
+            continue
+        s = l.strip()
+        if not s or s.startswith(";") or s.startswith(".") or s.endswith(":"):
+            continue
+        op = s.split()[0]
+        cur["ops"][op] += 1
+        cur["n"] += 1
+    blocks.append(cur)
+    return blocks
+
+
+def classify(op):
+    if op.startswith("v_mad_u64_u32"):
+        return "v_mad_u64_u32"
+    if op.startswith(("v_mul_lo", "v_mul_hi", "v_mul_u32", "v_mad_u32")):
+        return "v_mul32"
+    if op.startswith(("v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64", "v_lshl_or_b32")) or op.endswith("_b64"):
+        return "valu_64"
+    if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
+        return "vmem"
+    if op.startswith("ds_"):
+        return "lds"
+    if op.startswith("s_"):
+        return "salu/smem/branch"
+    if op.startswith("v_"):
+        return "valu_other"
+    return "other"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("asm")
+    ap.add_argument("symbol")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    lines = open(a.asm).read().splitlines()
+    name, body = function_body(lines, a.symbol)
+    blocks = blocks_of(body)
+    total = collections.Counter()
+    for b in blocks:
+        total.update(b["ops"])
+    print(f"{name}: {sum(total.values())} instructions, {total['v_mad_u64_u32']} v_mad_u64_u32 (static)")
+    loops = collections.OrderedDict()
+    for b in blocks:
+        if b["loop"]:
+            loops.setdefault(b["loop"], []).append(b)
+    out = {"function": name, "static_total": dict(total), "blocks": [], "loops": {}}
+    print(f"{'block':<14}{'loop':<12}{'d':>2}{'instr':>7}{'mad64':>7}{'valu':>7}{'vmem':>6}{'lds':>6}")
+    for b in blocks:
+        cls = collections.Counter()
+        for op, c in b["ops"].items():
+            cls[classify(op)] += c
+        valu = sum(v for k, v in cls.items() if k.startswith("v"))
+        print(f"{b['label']:<14}{str(b['loop']):<12}{b['depth']:>2}{b['n']:>7}{cls['v_mad_u64_u32']:>7}"
+              f"{cls['v_mad_u64_u32'] + cls['v_mul32'] + cls['valu_64'] + cls['valu_other']:>7}{cls['vmem']:>6}{cls['lds']:>6}")
+        out["blocks"].append({"label": b["label"], "loop": b["loop"], "depth": b["depth"], "instr": b["n"],
+                              "classes": dict(cls)})
+    for lp, bl in loops.items():
+        cls = collections.Counter()
+        for b in bl:
+            for op, c in b["ops"].items():
+                cls[classify(op)] += c
+        out["loops"][lp] = {"blocks": [b["label"] for b in bl], "classes": dict(cls)}
+        print(f"loop {lp}: {len(bl)} blocks, " + ", ".join(f"{k}={v}" for k, v in sorted(cls.items())))
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -42,7 +42,9 @@ extern "C" {
  *   std_coeff_proj_out   <- Haskell `msmStd` (G1/Proj.hs:228,262)
  *   _affine_out          <- bls12_381_G1_proj.c:654-670
  *   expos: npoints x expo_nlimbs u64 (Montgomery Fr for mont_coeff, plain integers for
- *   std_coeff, used verbatim -- no reduction mod r).  expo_nlimbs: 4 (mont), 1..4 (std).
+ *   std_coeff, used verbatim -- no reduction mod r).  expo_nlimbs: any >= 1; std scalars
+ *   are 64*expo_nlimbs-bit integers (G1_proj.c:511,552); for mont the first min(nl,4) limbs
+ *   of each row are the Montgomery value (the reference's result is undefined for nl != 4).
  *   grps : npoints affine points.  tgt: 3*NP (proj) or 2*NP (affine) u64. */
 ZKG_API void bn128_G1_proj_MSM_mont_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
 ZKG_API void bn128_G1_proj_MSM_std_coeff_proj_out(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_t *tgt, int expo_nlimbs);
@@ -252,8 +254,14 @@ ZKG_API double zkg_field_mul_rate(int field);
 /* MSM window heuristic used when window_size is not given */
 ZKG_API int zkg_msm_default_window(int npoints);
 
+/* per-phase HIP-event profile of every MSM call, printed to stderr (diagnostics) */
+ZKG_API void zkg_msm_profile(int on);
+/* test hook: cap on the sorted (window, point) entries one MSM pipeline pass handles
+ * (default and maximum 2^30; 0 restores it).  Larger MSMs run in window groups. */
+ZKG_API void zkg_msm_set_group_limit(size_t entries);
+
 /* timing probe of the dominant kernel (MSM bucket accumulation / NTT pass chain),
- * measured with HIP events on the library's own stream */
+ * measured with HIP events on each device's own stream; read sums over devices */
 ZKG_API void zkg_timer_enable(int on);
 ZKG_API void zkg_timer_reset(void);
 ZKG_API void zkg_timer_read(double *total_ms, long *launches);

@@ -173,6 +173,13 @@ class Reference:
             getattr(self.lib, name)(n, _p(scalars), _p(points), _p(res), nl)
         return res
 
+    def msm_jac(self, curve, scalars, points, mont=True):
+        """<C>_G1_jac_MSM_{mont,std}_coeff_jac_out (raw Jacobian output)"""
+        res = np.zeros(3 * NP[curve], dtype=np.uint64)
+        name = f"{curve}_G1_jac_MSM_{'mont' if mont else 'std'}_coeff_jac_out"
+        getattr(self.lib, name)(scalars.shape[0], _p(scalars), _p(points), _p(res), scalars.shape[1])
+        return res
+
     def ntt(self, curve, m, gen, src, inverse=False):
         out = np.zeros_like(src)
         name = f"{curve}_poly_mont_ntt_{'inverse' if inverse else 'forward'}"

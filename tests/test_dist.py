@@ -1,10 +1,12 @@
-"""Multi-rank MSM path on CPU: world_size 2 (and 4) over gloo.
+"""Multi-rank MSM path on CPU: world_size 2 (and 4) over gloo, through bench.py's own
+config-5 code path (bench.Dist + bench.sharded_msm_step + sharded.shard_range).
 
-Each rank computes the partial MSM of its contiguous shard (here with the oracle standing
-in for the per-GPU kernel -- the GPU kernel itself is covered by the -m gpu tests), the
-partials are exchanged with the same all-gather code bench.py uses over RCCL, and every
-rank combines them in rank order with the library's host-side point addition.  The
-result must equal the unsharded MSM bit for bit."""
+Each rank computes the partial MSM of its contiguous shard (here the oracle is injected in
+place of the per-GPU kernel, the only GPU-bound piece -- the kernel itself is covered by the
+-m gpu tests, including tests/test_gpu_dist.py which runs this path on the GPU), the
+partials are exchanged with the same all-gather bench.py uses over RCCL, and every rank
+combines them in rank order with the library's host-side point addition.  The result must
+equal the unsharded MSM bit for bit."""
 import os
 import socket
 import sys
@@ -26,22 +28,25 @@ def _free_port():
 def _worker(rank, world, port, curve, n_total, q):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
-    import torch.distributed as dist
+    from types import SimpleNamespace
+
+    import bench
     import zkalgebra as zk
     from oracle.oracle import Oracle
     from sharded import allgather_partials, combine_partials, shard_range
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist = bench.Dist(SimpleNamespace(backend="gloo"), device=0)
+    assert (dist.rank, dist.world) == (rank, world)
     lo, hi = shard_range(n_total, rank, world)
     sc = zk.gen_fr(curve, 0x5A4B0005, hi - lo, start=lo)
     pts = zk.gen_points(curve, 0x5A4B0005, hi - lo, start=lo)
     partial = Oracle().msm(curve, sc, pts, mont=True, out="proj")
-    parts = allgather_partials(partial)
-    proj, aff = combine_partials(curve, parts)
+    aff = bench.sharded_msm_step(zk, curve, hi - lo, None, None, 0, dist, msm_fn=lambda: partial)
+    proj, aff2 = combine_partials(curve, allgather_partials(partial))
+    assert (aff == aff2).all()
     q.put((rank, aff.tolist(), proj.tolist()))
-    dist.destroy_process_group()
+    dist.close()
 
 
 @pytest.mark.parametrize("world", [2, 4])

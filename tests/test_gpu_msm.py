@@ -20,12 +20,15 @@ def test_golden_affine_and_projective(gpu, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
-def test_golden_jacobian(gpu, oracle, curve):
+def test_golden_jacobian(gpu, reference, curve):
     NP = gpu.NLIMBS_P[curve]
     for name, sc, pts, mont, aff, projn in msm_cases(curve):
         jac = gpu.msm_jac(curve, sc, pts, std=not mont)
         if np.all(aff == np.uint64(0xFFFFFFFFFFFFFFFF)):
-            assert not jac[2 * NP:].any() and jac[:NP].any(), name   # (1:1:0)
+            # exactly the reference's Montgomery (1:1:0), G1_jac.c:182-187 (its MSM leaves
+            # the set_infinity value untouched when every term is infinity)
+            assert np.array_equal(jac, reference.msm_jac(curve, sc, pts, mont=mont)), name
+            assert not jac[2 * NP:].any() and np.array_equal(jac[:NP], jac[NP:2 * NP]), name
         else:
             assert np.array_equal(jac[:2 * NP], aff), name          # Z = 1 => (x, y)
 
@@ -124,3 +127,56 @@ def test_config5_bls12_381_msm_2_26_vs_reference(gpu):
         part = gpu.msm(curve, sc[k * step:(k + 1) * step], pts[k * step:(k + 1) * step])
         acc = part if acc is None else gpu.g1_add(curve, acc, part)
     assert [int(x) for x in gpu.g1_to_affine(curve, acc)] == cfg["affine"]
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("nl,high", [(5, "zero"), (5, "random"), (6, "random"), (9, "random")])
+def test_std_wide_scalars_vs_reference(gpu, reference, curve, nl, high):
+    """std coefficients of more than 4 limbs are used verbatim (G1_proj.c:511,552): the
+    reference accepts any expo_nlimbs -- so must we (256-bit slices, Horner on the host)"""
+    n = 300
+    rng = np.random.default_rng(nl * 10 + (high == "random"))
+    sc = np.zeros((n, nl), dtype=np.uint64)
+    sc[:, :4] = gpu.gen_fr(curve, 90 + nl, n)
+    if high == "random":
+        sc[:, 4:] = rng.integers(0, 2**63, size=(n, nl - 4), dtype=np.uint64) * np.uint64(2) + \
+            rng.integers(0, 2, size=(n, nl - 4), dtype=np.uint64)
+    pts = gpu.gen_points(curve, 91 + nl, n)
+    want = reference.msm(curve, sc, pts, mont=False)
+    assert np.array_equal(gpu.msm_affine(curve, sc, pts, std=True), want)
+    if high == "zero":
+        assert np.array_equal(want, gpu.msm_affine(curve, np.ascontiguousarray(sc[:, :4]), pts, std=True))
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("nl", [1, 2, 3, 5])
+def test_mont_other_nlimbs_does_not_abort(gpu, curve, nl):
+    """Montgomery coefficients with expo_nlimbs != 4: the reference's result is undefined
+    (Fr_mont_to_std reads 4 limbs per row, G1_proj.c:637-641); ours uses the row's first
+    min(nl, 4) limbs as the Montgomery value -- and, like the reference, does not abort"""
+    n = 500
+    base = gpu.gen_fr(curve, 95, n)
+    pts = gpu.gen_points(curve, 96, n)
+    sc = np.zeros((n, nl), dtype=np.uint64)
+    k = min(nl, 4)
+    sc[:, :k] = base[:, :k]
+    ext = np.zeros((n, 4), dtype=np.uint64)
+    ext[:, :k] = base[:, :k]
+    assert np.array_equal(gpu.msm_affine(curve, sc, pts), gpu.msm_affine(curve, ext, pts))
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("window,limit", [(4, 3 * 4000), (9, 4000), (16, 1)])
+def test_window_groups_vs_oracle(gpu, oracle, curve, window, limit):
+    """MSMs whose (window, point) entries exceed one pipeline pass (W n >= 2^30 by default:
+    int counts of the sort) run in window groups; the cap is lowered here to reach that path"""
+    n = 4000
+    sc = oracle.to_std(FR_FLD[curve], gpu.gen_fr(curve, 97, n))
+    pts = gpu.gen_points(curve, 98, n)
+    want = oracle.normalize(curve, oracle.msm(curve, sc, pts, mont=False, out="proj"))
+    try:
+        gpu.msm_set_group_limit(limit)
+        got = gpu.msm_variable(curve, sc, pts, window)
+    finally:
+        gpu.msm_set_group_limit(0)
+    assert np.array_equal(got, want)

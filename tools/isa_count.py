@@ -61,7 +61,7 @@ def classify(op):
         return "v_mad_u64_u32"
     if op.startswith(("v_mul_lo", "v_mul_hi", "v_mul_u32", "v_mad_u32")):
         return "v_mul32"
-    if op.startswith(("v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64", "v_lshl_or_b32")) or op.endswith("_b64"):
+    if op.startswith(("v_lshrrev_b64", "v_lshlrev_b64", "v_lshl_add_u64")) or op.endswith("_b64"):
         return "valu_64"
     if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
         return "vmem"
@@ -79,6 +79,7 @@ def main():
     ap.add_argument("asm")
     ap.add_argument("symbol")
     ap.add_argument("--json")
+    ap.add_argument("--note", default="", help="what one iteration of the hot loop is")
     a = ap.parse_args()
     lines = open(a.asm).read().splitlines()
     name, body = function_body(lines, a.symbol)
@@ -91,7 +92,7 @@ def main():
     for b in blocks:
         if b["loop"]:
             loops.setdefault(b["loop"], []).append(b)
-    out = {"function": name, "static_total": dict(total), "blocks": [], "loops": {}}
+    out = {"function": name, "note": a.note, "static_total": dict(total), "blocks": [], "loops": {}}
     print(f"{'block':<14}{'loop':<12}{'d':>2}{'instr':>7}{'mad64':>7}{'valu':>7}{'vmem':>6}{'lds':>6}")
     for b in blocks:
         cls = collections.Counter()
@@ -109,6 +110,17 @@ def main():
                 cls[classify(op)] += c
         out["loops"][lp] = {"blocks": [b["label"] for b in bl], "classes": dict(cls)}
         print(f"loop {lp}: {len(bl)} blocks, " + ", ".join(f"{k}={v}" for k, v in sorted(cls.items())))
+    if out["loops"]:
+        hot = max(out["loops"], key=lambda k: out["loops"][k]["classes"].get("v_mad_u64_u32", 0))
+        cls = out["loops"][hot]["classes"]
+        # issue-slot model (tools/microbench/valu_ceiling.hip, profiles/*valu_ceiling*.json):
+        # v_mad_u64_u32, v_mul_lo/hi_u32 and 64-bit shifts issue at half rate (1 slot),
+        # plain 32-bit VALU at full rate (1/2 slot); the chip's slot ceiling is the measured
+        # v_mad_u64_u32 rate
+        slots = cls.get("v_mad_u64_u32", 0) + cls.get("v_mul32", 0) + cls.get("valu_64", 0) + \
+            0.5 * cls.get("valu_other", 0)
+        out["hot_loop"] = {"label": hot, "per_iteration": cls, "issue_slots_per_iteration": slots}
+        print(f"hot loop {hot}: {slots:.1f} half-rate issue slots per iteration")
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
 

@@ -273,25 +273,13 @@ ZKG_API void zkg_fft_generator(int curve, int m, uint64_t *out) {
 
 ZKG_API int zkg_msm_default_window(int npoints) { return zk::msm_default_window(npoints); }
 
+ZKG_API void zkg_msm_profile(int on) { zk::msm_set_profile(on); }
+ZKG_API void zkg_msm_set_group_limit(size_t entries) { zk::msm_set_group_limit(entries); }
+
 ZKG_API double zkg_field_mul_rate(int field) { return zk::field_mul_rate(field); }
 
-ZKG_API void zkg_timer_enable(int on) {
-  KernelTimer &t = dominant_timer();
-  if (on && !t.ev0) {
-    ZK_CHECK(hipEventCreate(&t.ev0));
-    ZK_CHECK(hipEventCreate(&t.ev1));
-  }
-  t.enabled = on != 0;
-}
-ZKG_API void zkg_timer_reset(void) {
-  KernelTimer &t = dominant_timer();
-  t.total_ms = 0;
-  t.launches = 0;
-}
-ZKG_API void zkg_timer_read(double *total_ms, long *launches) {
-  KernelTimer &t = dominant_timer();
-  if (total_ms) *total_ms = t.total_ms;
-  if (launches) *launches = t.launches;
-}
+ZKG_API void zkg_timer_enable(int on) { timer_set_enabled(on != 0); }
+ZKG_API void zkg_timer_reset(void) { timer_reset_all(); }
+ZKG_API void zkg_timer_read(double *total_ms, long *launches) { timer_read_all(total_ms, launches); }
 
 }  // extern "C"

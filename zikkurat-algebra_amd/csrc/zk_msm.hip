@@ -21,6 +21,11 @@ int msm_default_window(int n) {
   return c;
 }
 
+void msm_set_profile(int on) { msm_profile_flag().store(on); }
+void msm_set_group_limit(size_t entries) {
+  msm_group_limit().store(entries == 0 || entries > MSM_MAX_GROUP_ENTRIES ? MSM_MAX_GROUP_ENTRIES : entries);
+}
+
 template void msm_g1<BN254>(int, const uint64_t *, int, const uint64_t *, bool, bool, int, uint64_t *);
 template void msm_g1<BLS381>(int, const uint64_t *, int, const uint64_t *, bool, bool, int, uint64_t *);
 

@@ -1,5 +1,6 @@
 // zk_msm.hpp -- C++ interface of the device MSM (used by the C ABI layer)
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 #include "zk_curve.hpp"
 #include "zk_host.hpp"
@@ -28,8 +29,10 @@ template <> struct HostOf<BLS381_G2> {
 };
 
 int msm_default_window(int n);
+void msm_set_profile(int on);  // per-phase event timing of every MSM call, printed to stderr
+void msm_set_group_limit(size_t entries);  // test hook: max sorted entries per pipeline pass (0: default)
 
-// scalars: n x nl u64 (nl in 1..4) (Montgomery Fr if mont, else plain 256-bit integers)
+// scalars: n x nl u64 (Montgomery Fr if mont, else plain integers of 64 nl bits, any nl >= 1)
 // points : n x 2*NP64 u64 affine Montgomery (all-0xFF = infinity)
 // out    : 3*NP64 u64 projective, reference Montgomery form, NOT normalised
 // host_inputs: pointers are host memory (staged by the call) vs device-resident

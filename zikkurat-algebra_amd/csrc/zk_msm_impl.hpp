@@ -32,6 +32,8 @@
 // wavefront's serial chain of 381-bit point adds is slow on CDNA4, so the
 // deep-but-narrow tail runs on one host core (step 9).
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <vector>
 #include "zk_curve.hpp"
@@ -74,20 +76,24 @@ __global__ void __launch_bounds__(256) k_points_int(const uint64_t *__restrict__
 
 // ---------------------------------------------------------------------------
 // 1. digits -> (key, value) pairs for the bucket sort.
+//    Scalar i is the integer in limbs [loff, loff + nread) of its `stride`-limb row (nread
+//    <= 4; longer std scalars are split into 256-bit slices by msm_g1).  Signed c-bit
+//    digits are computed for all windows (the carry runs through them) and the pairs of
+//    windows [wbase, wbase + Wg) are emitted, window-major, with local window w - wbase:
 //    key = w << c | (|digit| - 1), or w << c | B (sorts after every digit) for a zero
-//    digit; value = point index | sign << 31
+//    digit; value = point index | sign << 31 (n < 2^31 by the C ABI's int).
 template <class C>
-__global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int nl, int mont,
-                                                int c, int W, uint32_t *__restrict__ keys,
-                                                uint32_t *__restrict__ vals) {
+__global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int stride, int loff,
+                                                int nread, int mont, int c, int wbase, int Wg,
+                                                uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   using Fr = typename C::Fr;
   uint32_t k[9];
   {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {  // std scalars of 1..3 limbs: zero-extended
-      const uint64_t w = (j < nl) ? scalars[(size_t)i * nl + j] : 0;
+    for (int j = 0; j < 4; j++) {  // fewer than 4 limbs: zero-extended
+      const uint64_t w = (j < nread) ? scalars[(size_t)i * stride + loff + j] : 0;
       k[2 * j] = (uint32_t)w;
       k[2 * j + 1] = (uint32_t)(w >> 32);
     }
@@ -103,7 +109,8 @@ __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ sca
   const uint32_t full = 1u << c;
   const uint32_t mask = full - 1;
   uint32_t carry = 0;
-  for (int w = 0; w < W; w++) {
+  const int wend = wbase + Wg;
+  for (int w = 0; w < wend; w++) {
     uint32_t raw = (k[0] & mask) + carry;
     // shift the 256-bit scalar right by c (c < 32)
 #pragma unroll
@@ -118,14 +125,15 @@ __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ sca
       sign = 0;
       carry = 0;
     }
-    keys[(size_t)w * n + i] = ((uint32_t)w << c) | (mag ? mag - 1 : B);
-    vals[(size_t)w * n + i] = (uint32_t)i | sign;
+    if (w >= wbase) {
+      const uint32_t lw = (uint32_t)(w - wbase);
+      keys[(size_t)lw * n + i] = (lw << c) | (mag ? mag - 1 : B);
+      vals[(size_t)lw * n + i] = (uint32_t)i | sign;
+    }
   }
 }
 
-// 3. bucket offsets from the sorted keys: offsets[b] = first position whose rank is
-//    >= b, rank = digit * W + window (zero digits rank >= nb), one binary search per
-//    bucket (no serial loops, whatever the key distribution)
+// 3. bucket offsets from the sorted keys: rank = digit * W + window (zero digits rank >= nb)
 __device__ __forceinline__ uint32_t key_rank(uint32_t key, int c, uint32_t W) {
   return (key & ((1u << c) - 1)) * W + (key >> c);
 }
@@ -133,18 +141,6 @@ __device__ __forceinline__ uint32_t key_rank(uint32_t key, int c, uint32_t W) {
 __device__ __forceinline__ uint32_t bucket_slot(uint32_t b, uint32_t W, uint32_t B) {
   return (b % W) * B + b / W;
 }
-static __global__ void __launch_bounds__(256) k_offsets(const uint32_t *__restrict__ skeys, uint32_t M, uint32_t nb,
-                                                 int c, uint32_t W, uint32_t *__restrict__ offsets) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > nb) return;
-  uint32_t lo = 0, hi = M;  // first index in [lo, hi] with rank >= b
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (key_rank(skeys[mid], c, W) < b) lo = mid + 1; else hi = mid;
-  }
-  offsets[b] = lo;
-}
-
 // same offsets from one coalesced pass over the sorted keys: ranks are non-decreasing, so
 // entry e writes offsets[r] = e for every rank r in (rank(e-1), rank(e)] (clamped to nb;
 // zero digits rank >= nb), and the last entry fills the ranks after it with M
@@ -326,58 +322,6 @@ __global__ void __launch_bounds__(BS) k_stitch_blk(const uint32_t *__restrict__ 
   const uint32_t item_key = (cont_in || cont_out) ? key : nb;
   if (touches_start) okeys[2 * blk] = item_key;
   if (touches_end) okeys[2 * blk + 1] = touches_start ? nb : item_key;
-}
-
-// 5b. stitch level: the compacted items (sorted by key; payload e at vals[idx[e]]) are
-//     summed per key with the same balanced-chunk scheme; complete runs go to buckets[b], runs crossing a chunk
-//     boundary become the next level's items.  Levels repeat until one chunk remains.
-template <class C>
-__global__ void __launch_bounds__(256) k_stitch(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ idx,
-                                                const uint32_t *__restrict__ vals,
-                                                const uint32_t *__restrict__ count, uint32_t nb, int CH,
-                                                uint32_t W, uint32_t B, uint32_t *__restrict__ buckets, uint32_t *__restrict__ okeys,
-                                                uint32_t *__restrict__ ovals, uint32_t nslots) {
-  using F = typename C::Fp;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (2 * t >= nslots) return;
-  const uint32_t M = *count;
-  const uint32_t cs = t * (uint32_t)CH;
-  uint32_t k0 = nb, k1 = nb;
-  if (cs < M) {
-    const uint32_t ce = min(M, cs + (uint32_t)CH);
-    uint32_t b = keys[cs];
-    const bool cont_in = cs > 0 && keys[cs - 1] == b;
-    bool first_run = true;
-    Xyzz<F> acc;
-    xyzz_set_inf(acc);
-    for (uint32_t e = cs; e < ce; e++) {
-      const uint32_t k = keys[e];
-      if (k != b) {
-        if (first_run && cont_in) {
-          xyzz_store(ovals + (size_t)(2 * t) * xyzz_words<F>(), acc);
-          k0 = b;
-        } else {
-          xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
-        }
-        first_run = false;
-        xyzz_set_inf(acc);
-        b = k;
-      }
-      Xyzz<F> v;
-      xyzz_load(v, vals + (size_t)idx[e] * xyzz_words<F>());
-      xyzz_add(acc, v);
-    }
-    const bool cont_out = ce < M && keys[ce] == b;
-    if ((first_run && cont_in) || cont_out) {
-      const uint32_t slot = first_run ? 2 * t : 2 * t + 1;
-      xyzz_store(ovals + (size_t)slot * xyzz_words<F>(), acc);
-      if (first_run) k0 = b; else k1 = b;
-    } else {
-      xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
-    }
-  }
-  okeys[2 * t] = k0;
-  okeys[2 * t + 1] = k1;
 }
 
 // 5a'. index compaction: the valid item slots as (key, slot index) pairs -- the XYZZ
@@ -698,54 +642,6 @@ __global__ void __launch_bounds__(256) k_jobsum_quad(const uint32_t *__restrict_
     xyzz_store(out + ((size_t)w * c + j) * xyzz_words<F>(), acc);
 }
 
-// 7. weighted sums of the Y's by bits: per window, job (d, b) for b < l_d is
-//    U_{d,b} = sum_{v: bit b of v} Yd_v (2^(l_d - 1) items) and one job is sum_v Y0_v
-//    (2^l0 items); J = l0 + l1 + 1 = c jobs.  Same segment scheme: jobs ordered by
-//    length (total, then the l0 jobs over Y0, then the l1 jobs over Y1), G lanes each.
-//    Output P[w][j]: j = 0 total, 1..l0 -> (0, j-1), l0+1.. -> (1, j-1-l0).
-template <class C>
-__global__ void __launch_bounds__(256) k_jobsum(const uint32_t *__restrict__ Y, int W, int c, int l0, int QA,
-                                                int wlanes, uint32_t *__restrict__ out) {
-  using F = typename C::Fp;
-  const int l1 = c - 1 - l0;
-  const int NY = (1 << l0) + (1 << l1);
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  const int w = g / wlanes, t = g % wlanes;
-  const bool active = w < W;
-  // job j: length n_j, segment size G_j = clamp(n_j / QA, 1, 64); lane offset = prefix sum
-  int j = -1, G = 1, lane = 0, off = 0;  // padding lanes: no job, no fold
-  for (int jj = 0; jj < c; jj++) {
-    const int n = jj == 0 ? (1 << l0) : (jj <= l0 ? (1 << (l0 - 1)) : (1 << (l1 - 1)));
-    int Gj = n / QA;
-    Gj = Gj < 1 ? 1 : (Gj > 64 ? 64 : Gj);
-    if (t >= off && t < off + Gj) { j = jj; G = Gj; lane = t - off; }
-    off += Gj;
-  }
-  Xyzz<F> acc;
-  xyzz_set_inf(acc);
-  if (active && j >= 0) {
-    const int d = (j == 0 || j <= l0) ? 0 : 1;
-    const int b = j == 0 ? -1 : (d == 0 ? j - 1 : j - 1 - l0);
-    const int ld = d ? l1 : l0;
-    const int n = (b < 0) ? (1 << ld) : (1 << (ld - 1));
-    const int per = n / G;
-    const uint32_t *Yd = Y + ((size_t)w * NY + (d ? (1 << l0) : 0)) * xyzz_words<F>();
-    for (int k = 0; k < per; k++) {
-      const int e = lane * per + k;
-      int v = e;
-      if (b >= 0) {
-        const int lowmask = (1 << b) - 1;
-        v = ((e & ~lowmask) << 1) | (1 << b) | (e & lowmask);
-      }
-      Xyzz<F> p;
-      xyzz_load(p, Yd + (size_t)v * xyzz_words<F>());
-      xyzz_add(acc, p);
-    }
-  }
-  seg_fold(acc, G);
-  if (active && j >= 0 && lane == 0) xyzz_store(out + ((size_t)w * c + j) * xyzz_words<F>(), acc);
-}
-
 // export: XYZZ (device form) -> canonical reference-form coordinates, 4 x NP64 u64
 template <class C>
 __global__ void k_export(const uint32_t *__restrict__ in, int n, uint64_t *__restrict__ out) {
@@ -770,41 +666,34 @@ __global__ void k_export(const uint32_t *__restrict__ in, int n, uint64_t *__res
 // host orchestration
 
 struct MsmShape {
-  int n, c, W, B, l0, l1, NY, QY, J, CH, SCH, QA;
+  int n, c, W, B, l0, l1, NY, QY, J, CH, QA;  // W: windows handled by one pass of the pipeline
   SegRegion r0, r1;
-  int ylanes, jlanes;  // lanes per window of k_ysum / k_jobsum (multiples of 64)
+  int ylanes;  // lanes per window of k_ysum (multiple of 64)
 };
 
 static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; return r; }
 
-static int env_int(const char *name, int dflt) {
-  const char *v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
-}
-
-
-// bits: bit length bound of the scalars (255/254 for canonical Montgomery-path scalars
-// after REDC, 64*nl for std scalars, which are used verbatim).  Signed digits need
-// floor(bits/c) + 1 windows: the top window then holds at most c-1 bits plus the carry,
-// i.e. a digit <= 2^(c-1) = B, so no carry leaves it.
-static MsmShape make_shape(int n, int c, int bits) {
-  static const int envQY = env_int("ZK_MSM_QY", 0), envQA = env_int("ZK_MSM_QA", 0);
+// Shape of one pipeline pass over W windows of n scalars.  The constants were swept on
+// MI355X (round 1, profiles/r01_*): Y sums take 16 buckets per lane at scale, the weighted
+// job sums 8 items per lane, the accumulation 64 sorted entries per lane (128 from 2^25
+// entries on, profiles/r01_v7_ch_sweep.txt).
+static MsmShape make_shape(int n, int c, int W) {
   MsmShape s;
   s.n = n;
   s.c = c;
-  s.W = bits / c + 1;
+  s.W = W;
   s.B = 1 << (c - 1);
   s.l0 = c / 2;  // l0 + l1 = c - 1, l0 >= l1
   s.l1 = c - 1 - s.l0;
   s.NY = (1 << s.l0) + (1 << s.l1);
   auto pow2 = [](int v) { int r = 1; while (2 * r <= v) r *= 2; return r; };  // segments need powers of 2
-  // buckets per lane in the Y sums: 16 at scale (swept on MI355X), fewer when there are few
-  // buckets, so the sums keep ~64K lanes (2 W B bucket adds) instead of a long serial chain
+  // buckets per lane in the Y sums: 16 at scale, fewer when there are few buckets, so the
+  // sums keep ~64K lanes (2 W B bucket adds) instead of a long serial chain
   {
     const size_t adds = 2 * (size_t)s.W * (size_t)s.B;
     int q = (int)(adds >> 16);
     q = q < 1 ? 1 : (q > 16 ? 16 : q);
-    s.QY = envQY > 0 ? pow2(envQY) : pow2(q);
+    s.QY = pow2(q);
   }
   auto clampG = [](int g) { return g < 1 ? 1 : (g > 64 ? 64 : g); };
   s.r0 = SegRegion{1 << s.l1, clampG((1 << s.l0) / s.QY), 1 << s.l0};  // Y1 sums
@@ -817,65 +706,67 @@ static MsmShape make_shape(int n, int c, int bits) {
     const size_t ent = (size_t)s.W * (size_t)n;
     size_t ch = ent >> 17;
     s.CH = ch >= 64 ? 64 : (ch <= 4 ? 4 : (int)ch);
-    // from 2^25 entries on (BLS12-381 2^21+, BN128 2^21+) 128 per lane still leaves >= 2^18
-    // lanes and halves the partial items the stitch has to sum (MI355X sweep,
-    // profiles/r01_v7_ch_sweep.txt: BLS12-381 2^23 stitch 1.85 -> 0.76 ms, 25.0 -> 23.8 ms)
     if (ent >= ((size_t)1 << 25)) s.CH = 128;
-    static const int envCH = env_int("ZK_MSM_CH", 0);
-    if (envCH > 0) s.CH = envCH;
   }
-  static const int envSCH = env_int("ZK_MSM_SCH", 0);
-  s.SCH = envSCH >= 2 ? envSCH : 4;  // items per k_stitch thread (swept on MI355X: 4 < 8 < 16)
-  s.QA = envQA > 0 ? pow2(envQA) : 8;  // items per lane in the weighted job sums
-  s.jlanes = 0;
-  for (int j = 0; j < c; j++) {  // same job order / sizes as k_jobsum
-    const int n = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
-    s.jlanes += clampG(n / s.QA);
-  }
-  s.jlanes = (s.jlanes + 63) & ~63;
+  s.QA = 8;  // items per lane in the weighted job sums
   return s;
 }
 
-static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.n + s.CH - 1) / s.CH); }
-static size_t stitch_slots1(const MsmShape &s) { return 2 * ((stitch_slots0(s) + s.SCH - 1) / s.SCH) + 2; }
+// items per workgroup of the block stitch: 128 for the wide G2 points, so the LDS exchange
+// buffer stays at 64 KB
+template <class F>
+constexpr int stitch_bs() { return xyzz_words<F>() > 64 ? 128 : 256; }
 
+static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.n + s.CH - 1) / s.CH); }
+static size_t stitch_slots1(const MsmShape &s, int bs) { return 2 * ((stitch_slots0(s) + bs - 1) / bs) + 2; }
+
+// sorted entries of one pipeline pass: hipCUB takes int counts, offsets are u32
+constexpr size_t MSM_MAX_GROUP_ENTRIES = (size_t)1 << 30;
+// test hook (zkg_msm_set_group_limit): a smaller cap, so tests reach the multi-group path
+// at small sizes; 0 restores the default
+inline std::atomic<size_t> &msm_group_limit() {
+  static std::atomic<size_t> v{MSM_MAX_GROUP_ENTRIES};
+  return v;
+}
+
+// device bytes of the per-pass buffers
 template <class C>
-static size_t workspace_bytes(const MsmShape &s) {
+static size_t group_bytes(const MsmShape &s) {
   using F = typename C::Fp;
   const size_t xw = xyzz_words<F>() * 4;  // bytes per XYZZ
   const size_t nb = (size_t)s.W * s.B;
   const size_t maxent = (size_t)s.W * s.n;
-  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s);
+  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s, stitch_bs<F>());
   size_t cub = 0, cub2 = 0;
   ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                               (uint32_t *)nullptr, (uint32_t *)nullptr, (int)maxent, 0, s.c));
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)ns0));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-  add((size_t)s.n * 4 * 8);               // staged scalars (<= 4 limbs)
-  add((size_t)s.n * 2 * C::NP64 * 8);     // staged points
-  add((size_t)s.n * aff_words<F>() * 4);  // internal-form points
   add(maxent * 4 * 4);                    // keys, vals, sorted keys, sorted vals
   add((nb + 1) * 4);                      // offsets
   add(ns0 * (xw + 4) + ns0 * 16 + 64);    // level-0 items, compacted keys + index, flags, pos, count
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
-  add((size_t)s.W * s.NY * xw);              // Y
-  add((size_t)s.W * s.J * xw);               // per-(window, job) sums
-  add((size_t)s.W * s.J * 4 * C::NP64 * 8);    // export
+  add((size_t)s.W * s.NY * xw);           // Y
+  add((size_t)s.W * s.J * xw);            // per-(window, job) sums
+  add((size_t)s.W * s.J * 4 * C::NP64 * 8);  // export
   add(cub > cub2 ? cub : cub2);
   return bytes + (1 << 20);
 }
 
-// opt-in phase profile (env ZK_MSM_PROFILE=1): HIP events between the phases of one
-// call, printed to stderr with the host-side finish time.  Off by default.
+// Opt-in phase profile (zkg_msm_profile(1)): HIP events between the phases of every call,
+// printed to stderr with the host-side finish time.  Off by default.
+inline std::atomic<int> &msm_profile_flag() {
+  static std::atomic<int> on{0};
+  return on;
+}
 struct PhaseProf {
   bool on = false;
   hipStream_t st = nullptr;
   std::vector<std::pair<const char *, hipEvent_t>> ev;
   explicit PhaseProf(hipStream_t s) : st(s) {
-    static const int enabled = env_int("ZK_MSM_PROFILE", 0);
-    on = enabled != 0;
+    on = msm_profile_flag().load() != 0;
     mark("start");
   }
   void mark(const char *name) {
@@ -900,48 +791,34 @@ struct PhaseProf {
   }
 };
 
-template <class C>
-static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<typename HostOf<C>::Fp> &out);
+// Where the scalars of one pipeline run come from: row i holds `stride` u64 limbs, the
+// scalar is limbs [loff, loff + nread) (nread <= 4) -- Montgomery Fr or a plain integer
+struct ScalarSlice {
+  const uint64_t *data;
+  int stride, loff, nread;
+  bool mont;
+};
 
-// Run the device pipeline. scalars/points are DEVICE pointers (or host pointers when
-// host_inputs, in which case they are staged).  Result: projective point in
-// reference Montgomery form (not normalised), written to `out`.
+// One pass of the device pipeline over windows [wbase, wbase + s.W): digits, bucket sort,
+// accumulation, stitch, Y sums, job sums, export; the (window, job) sums land in the pinned
+// host buffer h (reference-form XYZZ, window-major).  Synchronises the stream.
 template <class C>
-static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs,
-                    bool mont, int window, zkh::Proj<typename HostOf<C>::Fp> &out) {
-  using HF = typename HostOf<C>::Fp;
+static void msm_group(Device &dev, const MsmShape &s, const ScalarSlice &sc, int wbase, const uint32_t *pts_int,
+                      uint64_t *h, uint32_t *hc, PhaseProf &prof) {
   using F = typename C::Fp;
-  if (n <= 0) {
-    zkh::proj_set_inf<HF>(out);
-    return;
-  }
-  const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
-  ZK_REQUIRE(nl >= 1 && nl <= 4, "msm: expo_nlimbs must be in 1..4 (scalars up to 256 bits)");
-  ZK_REQUIRE(!mont || nl == 4, "msm: Montgomery coefficients must have expo_nlimbs == 4");
-  MsmShape s = make_shape(n, c, mont ? HostOf<C>::Fr::BITS : 64 * nl);
+  const int n = s.n, c = s.c;
   const size_t nb = (size_t)s.W * s.B;
   const size_t xw = xyzz_words<F>();
   hipStream_t st = dev.stream;
-
-  dev.arena.reserve(workspace_bytes<C>(s));
-  dev.arena.reset();
-  const uint64_t *d_sc = scalars, *d_pt = points;
-  if (host_inputs) {
-    uint64_t *a = dev.arena.take<uint64_t>((size_t)n * nl);
-    uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
-    ZK_CHECK(hipMemcpyAsync(a, scalars, (size_t)n * nl * 8, hipMemcpyHostToDevice, st));
-    ZK_CHECK(hipMemcpyAsync(b, points, (size_t)n * 2 * C::NP64 * 8, hipMemcpyHostToDevice, st));
-    d_sc = a;
-    d_pt = b;
-  }
-  uint32_t *pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
   const size_t maxent = (size_t)s.W * n;
+  ZK_REQUIRE(maxent <= MSM_MAX_GROUP_ENTRIES, "msm: window group exceeds the sort capacity (internal sizing bug)");
   uint32_t *keys = dev.arena.take<uint32_t>(maxent);
   uint32_t *vals = dev.arena.take<uint32_t>(maxent);
   uint32_t *skeys = dev.arena.take<uint32_t>(maxent);
   uint32_t *list = dev.arena.take<uint32_t>(maxent);  // sorted values
   uint32_t *offsets = dev.arena.take<uint32_t>(nb + 1);
-  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s);
+  constexpr int STITCH_BS = stitch_bs<F>();
+  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s, STITCH_BS);
   uint32_t *ikeys0 = dev.arena.take<uint32_t>(ns0);
   uint32_t *ivals0 = dev.arena.take<uint32_t>(ns0 * xw);
   uint32_t *ckeys = dev.arena.take<uint32_t>(ns0);
@@ -964,63 +841,41 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   if (cub2 > cub) cub = cub2;
   void *cubtmp = dev.arena.take<char>(cub);
 
-  PhaseProf prof(st);
-  hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_pt, n, pts_int);
-  ZK_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_sc, n, nl, mont ? 1 : 0, c, s.W,
-                     keys, vals);
+  hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff, sc.nread,
+                     sc.mont ? 1 : 0, c, wbase, s.W, keys, vals);
   ZK_CHECK(hipGetLastError());
   prof.mark("digits");
   ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
   prof.mark("sort");
-  static const int offs_scan = env_int("ZK_MSM_OFFSCAN", 1);
-  if (offs_scan)
-    hipLaunchKernelGGL(k_offsets_scan, dim3(div_up(maxent, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
-                       (uint32_t)nb, c, (uint32_t)s.W, offsets);
-  else
-    hipLaunchKernelGGL(k_offsets, dim3(div_up(nb + 1, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
-                       (uint32_t)nb, c, (uint32_t)s.W, offsets);
+  hipLaunchKernelGGL(k_offsets_scan, dim3(div_up(maxent, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
+                     (uint32_t)nb, c, (uint32_t)s.W, offsets);
   ZK_CHECK(hipGetLastError());
-
   prof.mark("offsets");
-  KernelTimer &kt = dominant_timer();
-  {
-    if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev0, st));
-    // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
-    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(ns0 / 2, 256)), dim3(256), 0, st, pts_int, list, offsets,
-                       (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0, ivals0, (uint32_t)ns0);
-    ZK_CHECK(hipGetLastError());
-    if (kt.enabled) ZK_CHECK(hipEventRecord(kt.ev1, st));
-  }
+  const bool timed = wbase == 0;
+  if (timed) timer_begin(dev);
+  // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
+  hipLaunchKernelGGL(k_accum<C>, dim3(div_up(ns0 / 2, 256)), dim3(256), 0, st, pts_int, list, offsets,
+                     (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0, ivals0, (uint32_t)ns0);
+  ZK_CHECK(hipGetLastError());
+  if (timed) timer_end(dev);
   prof.mark("accum");
-  // stitch levels: compact the partial items, sum them per bucket, repeat
+  // stitch levels: compact the partial items, sum them per bucket (k_stitch_blk), repeat
   const uint32_t *inK = ikeys0, *inV = ivals0;
   size_t slots = ns0;
   uint32_t *outK = okA, *outV = ovA, *altK = okB, *altV = ovB;
-  // block stitch (k_stitch_blk, BS items per workgroup; 128 for the wide G2 points so the
-  // LDS exchange buffer stays at 64 KB) or the per-thread k_stitch (env ZK_MSM_STITCH_BLK=0)
-  constexpr int STITCH_BS = xyzz_words<F>() > 64 ? 128 : 256;
-  static const int stitch_blk = env_int("ZK_MSM_STITCH_BLK", 1);
-  const size_t stitch_chunk = stitch_blk ? (size_t)STITCH_BS : (size_t)s.SCH;
   auto stitch_level = [&]() -> bool {  // true: every item completed at this level
     hipLaunchKernelGGL(k_item_flags, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, (const uint32_t *)nullptr,
                        (uint32_t)slots, (uint32_t)nb, flags);
     ZK_CHECK(hipGetLastError());
     size_t cb = cub;
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, flags, pos, (int)slots, st));
-    const size_t chunk = stitch_chunk;
-    const bool final_level = slots <= chunk;  // all items fit one chunk: everything completes
-    const size_t nout = final_level ? 2 : 2 * ((slots + chunk - 1) / chunk);
+    const bool final_level = slots <= (size_t)STITCH_BS;  // all items fit one chunk: everything completes
+    const size_t nout = final_level ? 2 : 2 * ((slots + STITCH_BS - 1) / STITCH_BS);
     hipLaunchKernelGGL(k_item_index, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, flags, pos, (uint32_t)slots,
                        ckeys, cidx, ccount);
     ZK_CHECK(hipGetLastError());
-    if (stitch_blk) {
-      hipLaunchKernelGGL((k_stitch_blk<C, STITCH_BS>), dim3((unsigned)(nout / 2)), dim3(STITCH_BS), 0, st, ckeys, cidx, inV, ccount, (uint32_t)nb, (uint32_t)s.W,
-                         (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
-    } else {
-      hipLaunchKernelGGL(k_stitch<C>, dim3(div_up(nout / 2, 256)), dim3(256), 0, st, ckeys, cidx, inV, ccount,
-                         (uint32_t)nb, s.SCH, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
-    }
+    hipLaunchKernelGGL((k_stitch_blk<C, STITCH_BS>), dim3((unsigned)(nout / 2)), dim3(STITCH_BS), 0, st, ckeys, cidx,
+                       inV, ccount, (uint32_t)nb, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
     ZK_CHECK(hipGetLastError());
     inK = outK; inV = outV; slots = nout;
     uint32_t *tk = outK, *tv = outV;
@@ -1030,78 +885,57 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
   // Y sums, job sums, export and the copy back to the host
   const int ngrp = s.W * s.J;
   const size_t expbytes = (size_t)ngrp * 4 * C::NP64 * 8;
-  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(expbytes + 64));
-  uint32_t *hc = reinterpret_cast<uint32_t *>(h + ngrp * 4 * C::NP64);  // last stitch level's item count
   auto reduce_tail = [&]() {
-    static const int ys = env_int("ZK_MSM_YSUM", 2);  // 0: k_ysum, 1: k_ysum2, 2: k_ysum2 + data prefetch
     const int n0 = s.r0.count * s.r0.G, n1 = s.r1.count * s.r1.G;
-    if (ys && n0 % 256 == 0 && n1 % 256 == 0) {
+    if (n0 % 256 == 0 && n1 % 256 == 0) {  // block-level Y sums (every shape from c = 12 up)
       const unsigned nblk = (unsigned)(s.W * (n0 + n1) / 256);
-      if (ys == 2)
-        hipLaunchKernelGGL((k_ysum2<C, true>), dim3(nblk), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
-                           s.r1, Y);
-      else
-        hipLaunchKernelGGL((k_ysum2<C, false>), dim3(nblk), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
-                           s.r1, Y);
-    } else {
+      hipLaunchKernelGGL((k_ysum2<C, true>), dim3(nblk), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0, s.r1,
+                         Y);
+    } else {  // small shapes: in-wavefront segments
       const size_t lanes = (size_t)s.W * s.ylanes;
-      hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0,
-                         s.r0, s.r1, s.ylanes, Y);
+      hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
+                         s.r1, s.ylanes, Y);
     }
     ZK_CHECK(hipGetLastError());
     prof.mark("ysum");
-    static const int quad = env_int("ZK_MSM_QUAD", 1);
-    if (quad) {
-      int jl = 0;  // logical lanes per window, G <= 16
-      for (int j = 0; j < c; j++) {
-        const int nj = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
-        int g = nj / s.QA;
-        jl += g < 1 ? 1 : (g > 16 ? 16 : g);
-      }
-      const int wl = ((jl + 15) & ~15) * 4;
-      const size_t lanes = (size_t)s.W * wl;
-      hipLaunchKernelGGL(k_jobsum_quad<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, wl, P0);
-    } else {
-      const size_t lanes = (size_t)s.W * s.jlanes;
-      hipLaunchKernelGGL(k_jobsum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, s.jlanes, P0);
+    int jl = 0;  // logical lanes per window, G <= 16
+    for (int j = 0; j < c; j++) {
+      const int nj = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
+      int g = nj / s.QA;
+      jl += g < 1 ? 1 : (g > 16 ? 16 : g);
     }
+    const int wl = ((jl + 15) & ~15) * 4;
+    const size_t lanes = (size_t)s.W * wl;
+    hipLaunchKernelGGL(k_jobsum_quad<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, wl, P0);
     ZK_CHECK(hipGetLastError());
     prof.mark("jobsum");
     hipLaunchKernelGGL(k_export<C>, dim3(div_up(ngrp, 64)), dim3(64), 0, st, P0, ngrp, exp);
     ZK_CHECK(hipGetLastError());
     ZK_CHECK(hipMemcpyAsync(h, exp, expbytes, hipMemcpyDeviceToHost, st));
   };
-  // Levels 0 and 1 and the whole tail are enqueued without a host round trip: for
-  // well-spread scalars two levels complete every bucket.  Only when level 1 still leaves
-  // more than one chunk of items (skewed scalars) does the host run further levels and
-  // redo the tail.
-  static const int spec = env_int("ZK_MSM_SPEC", 3);  // levels enqueued before the first check
+  // Levels 0..2 and the whole tail are enqueued without a host round trip: for
+  // well-spread scalars they complete every bucket.  Only when level 2 still leaves more
+  // than one chunk of items (skewed scalars) does the host run further levels and redo the
+  // tail.
+  constexpr int SPECULATIVE_LEVELS = 3;
   bool done = false;
-  for (int lv = 0; lv < spec && !done; lv++) done = stitch_level();
+  for (int lv = 0; lv < SPECULATIVE_LEVELS && !done; lv++) done = stitch_level();
   prof.mark("stitch");
   if (!done) ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
   reduce_tail();
   ZK_CHECK(hipStreamSynchronize(st));
-  if (!done && *hc > (uint32_t)stitch_chunk) {
+  if (!done && *hc > (uint32_t)STITCH_BS) {
     for (;;) {
       if (stitch_level()) break;
       ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
       ZK_CHECK(hipStreamSynchronize(st));
-      if (*hc <= (uint32_t)stitch_chunk) break;  // this level's stitch had one chunk: all complete
+      if (*hc <= (uint32_t)STITCH_BS) break;  // this level's stitch had one chunk: all complete
     }
     reduce_tail();
     ZK_CHECK(hipStreamSynchronize(st));
   }
-  if (kt.enabled) {
-    float ms = 0;
-    ZK_CHECK(hipEventElapsedTime(&ms, kt.ev0, kt.ev1));
-    kt.total_ms += ms;
-    kt.launches++;
-  }
+  if (timed) timer_collect(dev);
   prof.mark("export");
-  const auto t0 = std::chrono::steady_clock::now();
-  finish_host<C>(s, h, out);
-  prof.report(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
 // host: combine the per-(window, job) sums (XYZZ, canonical reference form; job order
@@ -1112,16 +946,16 @@ static void msm_run(Device &dev, int n, const uint64_t *scalars, int nl, const u
 // c (W - 1) doublings is the only serial part.  On one host core a point op costs ~0.4 us
 // against ~20 us for a lone GPU lane, which is why this tail stays on the host.
 template <class C>
-static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<typename HostOf<C>::Fp> &out) {
+static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typename HostOf<C>::Fp> &out) {
   using HF = typename HostOf<C>::Fp;
   const int NP = C::NP64;
-  const int E = s.c - 1;  // local exponents 0 .. c-2
-  std::vector<zkh::Xyzz<HF>> V(s.W);
-  host_parallel_for(s.W, [&](int w) {
+  const int J = c, E = c - 1;  // local exponents 0 .. c-2
+  std::vector<zkh::Xyzz<HF>> V(W);
+  host_parallel_for(W, [&](int w) {
     std::vector<zkh::Xyzz<HF>> Z(E);
     for (auto &z : Z) zkh::xyzz_set_inf(z);
-    for (int j = 0; j < s.J; j++) {
-      const uint64_t *q = exported + ((size_t)w * s.J + j) * 4 * NP;
+    for (int j = 0; j < J; j++) {
+      const uint64_t *q = exported + ((size_t)w * J + j) * 4 * NP;
       zkh::Xyzz<HF> p;
       memcpy(p.X.v, q + 0 * NP, NP * 8);
       memcpy(p.Y.v, q + 1 * NP, NP * 8);
@@ -1139,29 +973,105 @@ static void finish_host(const MsmShape &s, const uint64_t *exported, zkh::Proj<t
     }
     V[w] = acc;
   });
-  zkh::Xyzz<HF> acc;
-  zkh::xyzz_set_inf(acc);
-  for (int w = s.W - 1; w >= 0; w--) {
-    for (int k = 0; k < s.c; k++) zkh::xyzz_dbl(acc, acc);
-    zkh::xyzz_add(acc, acc, V[w]);
+  zkh::xyzz_set_inf(out);
+  for (int w = W - 1; w >= 0; w--) {
+    for (int k = 0; k < c; k++) zkh::xyzz_dbl(out, out);
+    zkh::xyzz_add(out, out, V[w]);
   }
-  zkh::xyzz_to_proj(out, acc);
+}
+
+// Run the device pipeline for one scalar slice.  points are DEVICE pointers (or host
+// pointers when host_inputs, in which case they are staged, with the scalars).
+// Result: sum_i k_i P_i in host XYZZ (reference Montgomery form).
+template <class C>
+static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t *points, bool host_inputs,
+                    int window, zkh::Xyzz<typename HostOf<C>::Fp> &out) {
+  using F = typename C::Fp;
+  if (n <= 0) {
+    zkh::xyzz_set_inf(out);
+    return;
+  }
+  const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
+  const int bits = sc_in.mont ? HostOf<C>::Fr::BITS : 64 * sc_in.nread;
+  // Signed digits need floor(bits/c) + 1 windows: the top window then holds at most c-1
+  // bits plus the carry, i.e. a digit <= 2^(c-1) = B, so no carry leaves it.
+  const int W = bits / c + 1;
+  // window groups: one pipeline pass sorts at most MSM_MAX_GROUP_ENTRIES (W n >= 2^31 would
+  // overflow the sort's int count); n < 2^31 (int), so one window always fits
+  const int Wg = (int)std::min<size_t>((size_t)W, std::max<size_t>(1, msm_group_limit().load() / (size_t)n));
+  const MsmShape s = make_shape(n, c, Wg);
+  hipStream_t st = dev.stream;
+
+  const size_t sc_bytes = host_inputs ? (size_t)n * sc_in.stride * 8 : 0;
+  const size_t pt_bytes = host_inputs ? (size_t)n * 2 * C::NP64 * 8 : 0;
+  const size_t int_bytes = (size_t)n * aff_words<F>() * 4;
+  dev.arena.reserve(sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(s));
+  dev.arena.reset();
+  ScalarSlice sc = sc_in;
+  const uint64_t *d_pt = points;
+  if (host_inputs) {
+    uint64_t *a = dev.arena.take<uint64_t>((size_t)n * sc_in.stride);
+    uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
+    ZK_CHECK(hipMemcpyAsync(a, sc_in.data, sc_bytes, hipMemcpyHostToDevice, st));
+    ZK_CHECK(hipMemcpyAsync(b, points, pt_bytes, hipMemcpyHostToDevice, st));
+    sc.data = a;
+    d_pt = b;
+  }
+  uint32_t *pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
+  PhaseProf prof(st);
+  hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_pt, n, pts_int);
+  ZK_CHECK(hipGetLastError());
+  prof.mark("points");
+  const size_t mark = dev.arena.used();
+  const size_t per_w = (size_t)c * 4 * C::NP64;  // exported u64 per window
+  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging((size_t)W * per_w * 8 + 64));
+  uint32_t *hc = reinterpret_cast<uint32_t *>(h + (size_t)W * per_w);  // stitch item count
+  for (int wbase = 0; wbase < W; wbase += Wg) {
+    dev.arena.rewind(mark);
+    const MsmShape sg = (wbase + Wg <= W) ? s : make_shape(n, c, W - wbase);
+    msm_group<C>(dev, sg, sc, wbase, pts_int, h + (size_t)wbase * per_w, hc, prof);
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  finish_host<C>(c, W, h, out);
+  prof.report(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
 // ---------------------------------------------------------------------------
-// public (C++) entry points used by the C ABI layer
+// public (C++) entry point used by the C ABI layer
 
 template <class C>
 void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs, bool mont,
             int window, uint64_t *out_proj) {
   using HF = typename HostOf<C>::Fp;
+  ZK_REQUIRE(nl >= 1, "msm: expo_nlimbs must be >= 1");
   Device &dev = current_device();
   std::lock_guard<std::mutex> lock(dev.mu);
-  zkh::Proj<HF> r;
-  msm_run<C>(dev, n, scalars, nl, points, host_inputs, mont, window, r);
-  memcpy(out_proj + 0 * C::NP64, r.X.v, C::NP64 * 8);
-  memcpy(out_proj + 1 * C::NP64, r.Y.v, C::NP64 * 8);
-  memcpy(out_proj + 2 * C::NP64, r.Z.v, C::NP64 * 8);
+  zkh::Xyzz<HF> acc;
+  if (mont || nl <= 4) {
+    // Montgomery coefficients: the reference converts the first 4 limbs of each row
+    // (Fr_mont_to_std reads 4 limbs, G1_proj.c:637-641); for expo_nlimbs != 4 its result
+    // is undefined (it reads past the row / leaves limbs uninitialised), here the value of
+    // the row's first min(nl, 4) limbs is used
+    msm_run<C>(dev, n, ScalarSlice{scalars, nl, 0, nl < 4 ? nl : 4, mont}, points, host_inputs, window, acc);
+  } else {
+    // standard scalars wider than 256 bits, used verbatim like the reference
+    // (G1_proj.c:511,552): k = sum_j k_j 2^(256 j) over 4-limb slices, one device MSM per
+    // slice, combined by Horner on the host (256 doublings per slice)
+    zkh::xyzz_set_inf(acc);
+    const int nsl = (nl + 3) / 4;
+    for (int j = nsl - 1; j >= 0; j--) {
+      for (int k = 0; k < 256; k++) zkh::xyzz_dbl(acc, acc);
+      const int nread = nl - 4 * j < 4 ? nl - 4 * j : 4;
+      zkh::Xyzz<HF> r;
+      msm_run<C>(dev, n, ScalarSlice{scalars, nl, 4 * j, nread, false}, points, host_inputs, window, r);
+      zkh::xyzz_add(acc, acc, r);
+    }
+  }
+  zkh::Proj<HF> p;
+  zkh::xyzz_to_proj(p, acc);
+  memcpy(out_proj + 0 * C::NP64, p.X.v, C::NP64 * 8);
+  memcpy(out_proj + 1 * C::NP64, p.Y.v, C::NP64 * 8);
+  memcpy(out_proj + 2 * C::NP64, p.Z.v, C::NP64 * 8);
 }
 
 }  // namespace zk

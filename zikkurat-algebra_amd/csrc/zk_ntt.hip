@@ -515,7 +515,6 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   }
   uint64_t *scratch = dev.arena.take<uint64_t>(N * F::N64);
 
-  KernelTimer &kt = dominant_timer();
   size_t S = N, T = 1;
   const uint64_t *in = d_src;
   PassArgs pa;
@@ -546,22 +545,17 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     pa.last = last;
     pa.G = G;
     ZK_CHECK(hipFuncSetAttribute((const void *)k_ntt_pass<F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (kt.enabled && p == 0) ZK_CHECK(hipEventRecord(kt.ev0, st));
+    if (p == 0) timer_begin(dev);
     hipLaunchKernelGGL(k_ntt_pass<F>, dim3((unsigned)ntiles), dim3(NTT_THREADS), lds, st, in, out, pa, tw.inner_i[p],
                        tw.tab[p], last ? tw.scale : nullptr);
     ZK_CHECK(hipGetLastError());
-    if (kt.enabled && last) ZK_CHECK(hipEventRecord(kt.ev1, st));
+    if (last) timer_end(dev);
     in = out;
     T <<= r;
   }
   if (host_io) ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
   ZK_CHECK(hipStreamSynchronize(st));
-  if (kt.enabled) {
-    float ms = 0;
-    ZK_CHECK(hipEventElapsedTime(&ms, kt.ev0, kt.ev1));
-    kt.total_ms += ms;
-    kt.launches++;
-  }
+  timer_collect(dev);
 }
 
 void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst, bool host_io,

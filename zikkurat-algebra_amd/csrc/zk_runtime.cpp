@@ -1,8 +1,6 @@
 // zk_runtime.cpp -- per-device context: stream, grow-only arena, pinned staging.
 #include "zk_runtime.hpp"
 #include <atomic>
-#include <condition_variable>
-#include <thread>
 
 namespace zk {
 
@@ -53,72 +51,68 @@ Device &current_device() {
   return *g_devices[id];
 }
 
-namespace {
-struct HostPool {
-  std::mutex run_mu;  // one job at a time
-  std::mutex mu;
-  std::condition_variable cv;
-  uint64_t gen = 0;
-  const std::function<void(int)> *fn = nullptr;
-  int n = 0;
-  std::atomic<int> next{0}, done{0};
-  int workers = 0;
-  HostPool() {
-    unsigned hw = std::thread::hardware_concurrency();
-    workers = hw > 2 ? (int)(hw - 1 < 7 ? hw - 1 : 7) : 0;
-    for (int i = 0; i < workers; i++) std::thread([this] { loop(); }).detach();
-  }
-  void drain() {
-    for (;;) {
-      const int i = next.fetch_add(1);
-      if (i >= n) break;
-      (*fn)(i);
-      done.fetch_add(1);
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return gen != seen; });
-        seen = gen;
-      }
-      drain();
-    }
-  }
-  void run(int count, const std::function<void(int)> &f) {
-    std::lock_guard<std::mutex> g(run_mu);
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      fn = &f;
-      n = count;
-      next = 0;
-      done = 0;
-      gen++;
-    }
-    cv.notify_all();
-    drain();
-    while (done.load() < count) std::this_thread::yield();
-    std::lock_guard<std::mutex> lk(mu);
-    n = 0;  // late-waking workers find nothing to do
-  }
-};
-}  // namespace
+// ---------------------------------------------------------------------------- kernel timer
+static std::atomic<bool> g_timer_on{false};
 
-void host_parallel_for(int n, const std::function<void(int)> &fn) {
-  if (n <= 0) return;
-  static HostPool *pool = new HostPool();  // leaked on purpose: detached workers outlive static teardown
-  if (n == 1 || pool->workers == 0) {
-    for (int i = 0; i < n; i++) fn(i);
+void timer_set_enabled(bool on) { g_timer_on.store(on); }
+
+void timer_begin(Device &dev) {
+  if (!g_timer_on.load()) {
+    dev.timer.armed = false;
     return;
   }
-  pool->run(n, fn);
+  if (!dev.timer.ev0) {  // created on the device whose stream records them (the caller's)
+    ZK_CHECK(hipEventCreate(&dev.timer.ev0));
+    ZK_CHECK(hipEventCreate(&dev.timer.ev1));
+  }
+  dev.timer.armed = true;
+  ZK_CHECK(hipEventRecord(dev.timer.ev0, dev.stream));
 }
 
-KernelTimer &dominant_timer() {
-  static KernelTimer t;
-  return t;
+void timer_end(Device &dev) {
+  if (dev.timer.armed) ZK_CHECK(hipEventRecord(dev.timer.ev1, dev.stream));
+}
+
+void timer_collect(Device &dev) {
+  if (!dev.timer.armed) return;
+  float ms = 0;
+  ZK_CHECK(hipEventSynchronize(dev.timer.ev1));
+  ZK_CHECK(hipEventElapsedTime(&ms, dev.timer.ev0, dev.timer.ev1));
+  dev.timer.total_ms += ms;
+  dev.timer.launches++;
+  dev.timer.armed = false;
+}
+
+void timer_reset_all() {
+  std::vector<Device *> devs;
+  {
+    std::lock_guard<std::mutex> lock(g_devices_mu);
+    devs = g_devices;
+  }
+  for (Device *d : devs)
+    if (d) {
+      std::lock_guard<std::mutex> lock(d->mu);
+      d->timer.total_ms = 0;
+      d->timer.launches = 0;
+    }
+}
+
+void timer_read_all(double *total_ms, long *launches) {
+  std::vector<Device *> devs;
+  {
+    std::lock_guard<std::mutex> lock(g_devices_mu);
+    devs = g_devices;
+  }
+  double t = 0;
+  long n = 0;
+  for (Device *d : devs)
+    if (d) {
+      std::lock_guard<std::mutex> lock(d->mu);
+      t += d->timer.total_ms;
+      n += d->timer.launches;
+    }
+  if (total_ms) *total_ms = t;
+  if (launches) *launches = n;
 }
 
 }  // namespace zk

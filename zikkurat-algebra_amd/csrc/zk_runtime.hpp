@@ -14,6 +14,7 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include "zk_hostpool.hpp"
 
 namespace zk {
 
@@ -35,6 +36,7 @@ class Arena {
  public:
   void reserve(size_t bytes);  // grows (re-allocates) only when larger than current
   void reset() { off_ = 0; }
+  void rewind(size_t off) { off_ = off; }  // release everything taken after used() == off
   template <class T>
   T *take(size_t count) {
     size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
@@ -52,6 +54,16 @@ class Arena {
   size_t off_ = 0;
 };
 
+// Timing probe of the dominant kernel (MSM bucket accumulation / NTT pass chain), used by
+// bench.py.  Per device: its events belong to that device and are only touched while the
+// device's mutex is held (every MSM / NTT call holds it).
+struct KernelTimer {
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool armed = false;  // this call recorded ev0
+  double total_ms = 0;
+  long launches = 0;
+};
+
 struct Device {
   int id = 0;
   hipStream_t stream = nullptr;
@@ -61,25 +73,19 @@ struct Device {
   void *pinned = nullptr;
   size_t pinned_cap = 0;
   void *host_staging(size_t bytes);
+  KernelTimer timer;
 };
 
 // The device of the calling thread (hipGetDevice), lazily initialised.
 Device &current_device();
 
-// simple kernel timing probe used by bench.py: the last launch of the named
-// "dominant" kernel family records its duration here (ms) when enabled.
-struct KernelTimer {
-  bool enabled = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  double total_ms = 0;
-  long launches = 0;
-};
-KernelTimer &dominant_timer();
-
-// Small persistent host thread pool for the serial-on-GPU tails that split into
-// independent pieces (e.g. the MSM's per-window Horner segments).  run() is
-// synchronous; the calling thread works too.  Calls from several threads serialise.
-void host_parallel_for(int n, const std::function<void(int)> &fn);
+// kernel timer (caller holds dev.mu for begin/end/collect)
+void timer_set_enabled(bool on);
+void timer_begin(Device &dev);    // records ev0 on dev.stream when the timer is enabled
+void timer_end(Device &dev);      // records ev1
+void timer_collect(Device &dev);  // after the stream is synchronised: accumulate ev1 - ev0
+void timer_reset_all();
+void timer_read_all(double *total_ms, long *launches);
 
 inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 

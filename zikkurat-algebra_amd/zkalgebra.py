@@ -59,6 +59,7 @@ EXTENSION_SYMBOLS = [
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
     "zkg_field_mul_rate", "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
     "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
+    "zkg_msm_profile", "zkg_msm_set_group_limit",
 ]
 
 _lib = None
@@ -84,6 +85,7 @@ def load():
         lib.zkg_gen_fr.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, U64P]
         lib.zkg_gen_g1_points.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, U64P]
         lib.zkg_timer_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]
+        lib.zkg_msm_set_group_limit.argtypes = [ctypes.c_size_t]
         lib.zkg_field_mul_rate.restype = ctypes.c_double
         lib.zkg_field_mul_rate.argtypes = [ctypes.c_int]
         for c in CURVES:
@@ -147,6 +149,8 @@ def _check_msm(curve, coeffs, points):
         raise ValueError("msm: incompatible array dimensions")   # G1/Proj.hs:239
     if points.shape[1] != 2 * NLIMBS_P[curve]:
         raise ValueError("msm: points must be affine (x, y) in Montgomery form")
+    if coeffs.shape[1] < 1:
+        raise ValueError("msm: coefficients need at least one limb")
 
 
 def msm(curve, coeffs, points):
@@ -517,11 +521,21 @@ class DeviceBuffer:
             self.ptr = None
 
 
-def msm_device(curve, n, d_scalars, d_points, mont=True, window=0):
+def msm_device(curve, n, d_scalars, d_points, mont=True, window=0, nlimbs=4):
     out = np.zeros(3 * NLIMBS_P[curve], dtype=np.uint64)
-    load().zkg_g1_msm_device(CURVE_ID[curve], n, d_scalars.ptr, 4, 1 if mont else 0, d_points.ptr, _p(out),
+    load().zkg_g1_msm_device(CURVE_ID[curve], n, d_scalars.ptr, nlimbs, 1 if mont else 0, d_points.ptr, _p(out),
                              window)
     return out
+
+
+def msm_profile(on):
+    """per-phase HIP-event timing of every MSM call, printed to stderr"""
+    load().zkg_msm_profile(1 if on else 0)
+
+
+def msm_set_group_limit(entries):
+    """test hook: max sorted entries per MSM pipeline pass (0 = default 2^30)"""
+    load().zkg_msm_set_group_limit(int(entries))
 
 
 def arr_op_device(curve, op, n, d_a, d_b=None, d_c=None, kA=None, kB=None, d_tgt=None):

@@ -9,17 +9,19 @@
 #   prof      rocprofv3 --kernel-trace --stats of a short bench -> gpurun_out/TAG_prof/
 #   pmcf      rocprofv3 --pmc FETCH_SIZE (own pass) -> gpurun_out/TAG_pmcf/
 #   pmcw      rocprofv3 --pmc WRITE_SIZE (own pass) -> gpurun_out/TAG_pmcw/
+#   pmcsq     rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU ... (VALU issue, own pass) -> gpurun_out/TAG_pmcsq/
+#   listpmc   rocprofv3 -L (available counters)   -> gpurun_out/TAG_counters.txt
 #   ceiling   tools/microbench/valu_ceiling (prebuilt) -> gpurun_out/TAG_ceiling.json
 #   ext       tools/bench_ext.py                  -> gpurun_out/TAG_ext.json
 #   phases    MSM phase profile at several sizes  -> gpurun_out/TAG_phases.txt
-#   cmd       the command in $JOB_CMD             -> gpurun_out/TAG_cmd.log
+#   cmd       bash tools/job_cmd.sh (scratch commands of the current experiment) -> gpurun_out/TAG_cmd.log
 set -o pipefail
 TAG=$1
 shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 O=gpurun_out/$TAG
-BENCH_SHORT="bench.py --steps 5 --warmup 2 --no-cpu-baseline --ntt-steps 3"
+BENCH_SHORT="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --ntt-steps 3"
 for step in "$@"; do
   echo "[$(date +%T)] step $step"
   case $step in
@@ -34,10 +36,13 @@ for step in "$@"; do
               > /dev/null 2> ${O}_pmcf.err ;;
     pmcw) timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d ${O}_pmcw -o run --output-format csv -- python3 $BENCH_SHORT \
               > /dev/null 2> ${O}_pmcw.err ;;
+    pmcsq) timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+              -d ${O}_pmcsq -o run --output-format csv -- python3 $BENCH_SHORT > /dev/null 2> ${O}_pmcsq.err ;;
+    listpmc) timeout -k 10 120 rocprofv3 -L > ${O}_counters.txt 2>&1 ;;
     ceiling) timeout -k 10 120 tools/microbench/valu_ceiling > ${O}_ceiling.json 2> ${O}_ceiling.err ;;
     ext) timeout -k 10 400 python -u tools/bench_ext.py > ${O}_ext.json 2> ${O}_ext.err ;;
     phases) timeout -k 10 300 python -u tools/sweep_window.py phases > ${O}_phases.txt 2>&1 ;;
-    cmd) timeout -k 10 ${JOB_TIMEOUT:-300} bash -c "$JOB_CMD" > ${O}_cmd.log 2>&1 ;;
+    cmd) timeout -k 10 ${JOB_TIMEOUT:-400} bash tools/job_cmd.sh > ${O}_cmd.log 2>&1 ;;
     *) echo "unknown step $step"; false ;;
   esac
   rc=$?

@@ -7,30 +7,27 @@
 // identical for points outside the order-r subgroup too), computed with
 // a GPU-shaped schedule:
 //
-//   0. k_points_int affine points -> internal radix (one product per coordinate)
-//   1. k_digits     scalar (Montgomery -> standard by REDC, Fr_mont.c:330-335) ->
-//                   signed c-bit digits for all W windows -> (key, index|sign), key =
-//                   window << c | (|digit| - 1); keys are emitted window-major
-//   2. sort         LSD radix sort of the W*n pairs on the c in-window bits only
-//                   (hipCUB onesweep, 2 passes at c = 16): the sort is stable, so
-//                   equal digits stay window-major and every (window, digit) bucket is
-//                   one contiguous run, ordered by rank = digit * W + window
-//   3. k_offsets    bucket start offsets (per rank) from the sorted keys
-//   4. k_accum      balanced bucket accumulation: every thread adds exactly CH
-//                   consecutive sorted entries (mixed XYZZ += affine adds), flushing
-//                   complete runs to their bucket and boundary runs as partial items
-//   5. k_stitch     partial items are compacted and summed per bucket with the same
-//                   balanced scheme, level after level (log_{SCH/2} levels): no serial
-//                   loop anywhere, so skewed scalars (all equal, carry windows) stay fast
-//   6. k_seg        per (window, segment of L buckets): T = sum B_m, R = sum (m-lo+1) B_m
-//   7. k_jobsum     sum_m m B_m = sum_s R_s + L * sum_k 2^k U_k, U_k = sum_{s: bit k} T_s:
-//                   every term is a plain point sum; one workgroup per (window, job)
-//                   with an LDS tree
-//   9. host         Horner over the power-of-two exponents, normalise / to_affine
+//   0. k_points_int   affine points -> internal radix (one product per coordinate)
+//   1. k_digits       scalar (Montgomery -> standard by REDC, Fr_mont.c:330-335) ->
+//                     signed c-bit digits of every window
+//      k_bucket_lds   bucket sort of the (window, point) entries: LDS counting sort per
+//                     (window, chunk) workgroup -> bucket offsets + bucket-ordered list
+//                     of point index | sign (hipCUB radix sort when c > 16);
+//                     bucket rank = window * B + |digit| - 1
+//   2. k_accum        balanced bucket accumulation: every thread adds exactly CH
+//                     consecutive list entries (mixed XYZZ += affine adds), flushing
+//                     complete runs to their bucket and boundary runs as partial items
+//   3. k_stitch_blk   partial items are compacted and summed per bucket by block-level
+//                     segmented scans, level after level: no serial loop anywhere, so
+//                     skewed scalars (all equal, carry windows) stay fast
+//   4. k_ysum(2)      digit split of the bucket weights into plain sums Y0, Y1
+//   5. k_jobsum_quad  the weighted Y sums by bit jobs (quad-cooperative additions)
+//   6. host           Horner over the power-of-two exponents and the windows
+// Windows are processed in groups when W n exceeds one pass's sort capacity.
 //
 // Every phase is wide (>= ~1e5 threads at 2^20) except the last tiny levels: a lone
 // wavefront's serial chain of 381-bit point adds is slow on CDNA4, so the
-// deep-but-narrow tail runs on one host core (step 9).
+// deep-but-narrow tail runs on the host (step 6).
 #include <hipcub/hipcub.hpp>
 #include <algorithm>
 #include <atomic>
@@ -75,22 +72,18 @@ __global__ void __launch_bounds__(256) k_points_int(const uint64_t *__restrict__
 }
 
 // ---------------------------------------------------------------------------
-// 1. digits -> (key, value) pairs for the bucket sort.
+// 1. Signed c-bit digits of one scalar, window by window.
 //    Scalar i is the integer in limbs [loff, loff + nread) of its `stride`-limb row (nread
-//    <= 4; longer std scalars are split into 256-bit slices by msm_g1).  Signed c-bit
-//    digits are computed for all windows (the carry runs through them) and the pairs of
-//    windows [wbase, wbase + Wg) are emitted, window-major, with local window w - wbase:
-//    key = w << c | (|digit| - 1), or w << c | B (sorts after every digit) for a zero
-//    digit; value = point index | sign << 31 (n < 2^31 by the C ABI's int).
+//    <= 4; longer std scalars are split into 256-bit slices by msm_g1), converted from
+//    Montgomery form first when `mont` (REDC, Fr_mont.c:330-335).  A digit is raw - 2^c
+//    (negative) when raw = bits + carry > 2^(c-1), so |digit| <= 2^(c-1) = B.
 template <class C>
-__global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int stride, int loff,
-                                                int nread, int mont, int c, int wbase, int Wg,
-                                                uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  using Fr = typename C::Fr;
+struct DigitStream {
   uint32_t k[9];
-  {
+  uint32_t carry;
+  __device__ __forceinline__ void load(const uint64_t *__restrict__ scalars, int i, int stride, int loff, int nread,
+                                       int mont) {
+    using Fr = typename C::Fr;
 #pragma unroll
     for (int j = 0; j < 4; j++) {  // fewer than 4 limbs: zero-extended
       const uint64_t w = (j < nread) ? scalars[(size_t)i * stride + loff + j] : 0;
@@ -98,59 +91,113 @@ __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ sca
       k[2 * j + 1] = (uint32_t)(w >> 32);
     }
     k[8] = 0;
-    if (mont) {  // Montgomery -> standard (REDC), Fr_mont.c:330-335
+    if (mont) {
       Fe<Fr> s, t;
       fe_unpack(s, k);
       fe_ref_to_std(t, s);
       fe_pack(k, t);
     }
+    carry = 0;
   }
-  const uint32_t B = 1u << (c - 1);
-  const uint32_t full = 1u << c;
-  const uint32_t mask = full - 1;
-  uint32_t carry = 0;
-  const int wend = wbase + Wg;
-  for (int w = 0; w < wend; w++) {
-    uint32_t raw = (k[0] & mask) + carry;
-    // shift the 256-bit scalar right by c (c < 32)
+  // next window's |digit| (0 .. B) and sign (0x80000000 for negative)
+  __device__ __forceinline__ uint32_t next(int c, uint32_t &sign) {
+    const uint32_t full = 1u << c, B = full >> 1;
+    const uint32_t raw = (k[0] & (full - 1)) + carry;
 #pragma unroll
-    for (int j = 0; j < 8; j++) k[j] = __builtin_amdgcn_alignbit(k[j + 1], k[j], c);
-    uint32_t mag, sign;
+    for (int j = 0; j < 8; j++) k[j] = __builtin_amdgcn_alignbit(k[j + 1], k[j], c);  // >>= c (c < 32)
     if (raw > B) {  // negative digit raw - 2^c (zero when raw == 2^c)
-      mag = full - raw;
       sign = 0x80000000u;
       carry = 1;
-    } else {
-      mag = raw;
-      sign = 0;
-      carry = 0;
+      return full - raw;
     }
-    if (w >= wbase) {
-      const uint32_t lw = (uint32_t)(w - wbase);
-      keys[(size_t)lw * n + i] = (lw << c) | (mag ? mag - 1 : B);
+    sign = 0;
+    carry = 0;
+    return raw;
+  }
+};
+
+// 2. Bucket sort of the (window, point) entries.  Buckets are ranked window-major:
+//    rank = (w - wbase) * B + |digit| - 1 over the windows [wbase, wbase + Wg) of this
+//    pipeline pass (B = 2^(c-1) buckets per window); zero digits belong to no bucket.  The
+//    result is the bucket offsets (nb + 1 entries, offsets[nb] = total) and the
+//    bucket-ordered list of point index | sign << 31 (n < 2^31 by the C ABI's int).
+//
+//    c <= 16 (B <= 32768, the 2^10..2^24 shapes): LDS counting sort.  k_digits writes one
+//    u32 per entry (|digit| | sign, window-major); a workgroup owns M entries of ONE window,
+//    counts them in an LDS histogram of its window's B buckets (LDS atomics), and adds the
+//    histogram to the global counts with one coalesced atomic per nonzero bucket; an
+//    exclusive scan gives the offsets; the scatter pass recounts, claims each bucket's slot
+//    range with one atomic per nonzero bucket and hands out slots from LDS.  Global traffic
+//    is ~4 passes of 4 B per entry, and only B atomics per workgroup reach L2 (random
+//    per-entry global atomics measured 5-10x slower).  The order inside a bucket depends on
+//    atomic timing; bucket sums are group sums, so the canonical result does not.
+//    c > 16: hipCUB radix sort of (rank, value) pairs on ceil(log2(nb + 1)) bits.
+template <class C, bool KEYS>
+__global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int stride, int loff,
+                                                int nread, int mont, int c, int wbase, int Wg,
+                                                uint32_t *__restrict__ out, uint32_t *__restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DigitStream<C> ds;
+  ds.load(scalars, i, stride, loff, nread, mont);
+  const uint32_t B = 1u << (c - 1);
+  const uint32_t nb = (uint32_t)Wg * B;
+  for (int w = 0; w < wbase + Wg; w++) {
+    uint32_t sign;
+    const uint32_t mag = ds.next(c, sign);
+    if (w < wbase) continue;
+    const uint32_t lw = (uint32_t)(w - wbase);
+    if (KEYS) {  // (rank | nb for zero digits, value) pairs for the radix sort
+      out[(size_t)lw * n + i] = mag ? lw * B + mag - 1 : nb;
       vals[(size_t)lw * n + i] = (uint32_t)i | sign;
+    } else {
+      out[(size_t)lw * n + i] = mag | sign;
     }
   }
 }
 
-// 3. bucket offsets from the sorted keys: rank = digit * W + window (zero digits rank >= nb)
-__device__ __forceinline__ uint32_t key_rank(uint32_t key, int c, uint32_t W) {
-  return (key & ((1u << c) - 1)) * W + (key >> c);
+// Workgroup (window w = blockIdx.y, entries [blockIdx.x * M, +M)) LDS histogram; the SCATTER
+// pass writes the list, the counting pass adds into `ctr` (counts).
+template <bool SCATTER>
+__global__ void __launch_bounds__(1024) k_bucket_lds(const uint32_t *__restrict__ dig, int n, int M, int c,
+                                                     uint32_t *__restrict__ ctr, uint32_t *__restrict__ list) {
+  extern __shared__ uint32_t hist[];
+  const uint32_t B = 1u << (c - 1);
+  const uint32_t w = blockIdx.y;
+  const int e0 = blockIdx.x * M, e1 = min(n, e0 + M);
+  const uint32_t *d = dig + (size_t)w * n;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  for (int e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+    const uint32_t mag = d[e] & 0x7fffffffu;
+    if (mag) atomicAdd(&hist[mag - 1], 1u);
+  }
+  __syncthreads();
+  uint32_t *g = ctr + (size_t)w * B;
+  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) {
+    const uint32_t h = hist[b];
+    if (!h) continue;
+    if (SCATTER) hist[b] = atomicAdd(&g[b], h);  // this workgroup's slot range in bucket b
+    else atomicAdd(&g[b], h);
+  }
+  if (!SCATTER) return;
+  __syncthreads();
+  for (int e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+    const uint32_t v = d[e];
+    const uint32_t mag = v & 0x7fffffffu;
+    if (mag) list[atomicAdd(&hist[mag - 1], 1u)] = (uint32_t)e | (v & 0x80000000u);
+  }
 }
-// storage slot of the bucket with rank b (window-major: w * B + digit)
-__device__ __forceinline__ uint32_t bucket_slot(uint32_t b, uint32_t W, uint32_t B) {
-  return (b % W) * B + b / W;
-}
-// same offsets from one coalesced pass over the sorted keys: ranks are non-decreasing, so
-// entry e writes offsets[r] = e for every rank r in (rank(e-1), rank(e)] (clamped to nb;
-// zero digits rank >= nb), and the last entry fills the ranks after it with M
+
+// offsets from the radix-sorted ranks (nondecreasing; zero digits rank nb): entry e writes
+// offsets[r] = e for every rank r in (rank(e-1), rank(e)], the last entry fills the ranks
+// after it with M
 static __global__ void __launch_bounds__(256) k_offsets_scan(const uint32_t *__restrict__ skeys, uint32_t M,
-                                                             uint32_t nb, int c, uint32_t W,
-                                                             uint32_t *__restrict__ offsets) {
+                                                             uint32_t nb, uint32_t *__restrict__ offsets) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= M) return;
-  const uint32_t r = min(key_rank(skeys[e], c, W), nb);
-  const uint32_t lo = e ? min(key_rank(skeys[e - 1], c, W), nb) + 1 : 0;
+  const uint32_t r = min(skeys[e], nb);
+  const uint32_t lo = e ? min(skeys[e - 1], nb) + 1 : 0;
   for (uint32_t q = lo; q <= r; q++) offsets[q] = e;
   if (e == M - 1)
     for (uint32_t q = r + 1; q <= nb; q++) offsets[q] = M;
@@ -166,25 +213,62 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ offse
   return lo;
 }
 
-// 4. level-0 balanced accumulation: thread t owns sorted entries [t*CH, min((t+1)*CH, total)).
+// 4. level-0 balanced accumulation: thread t owns list entries [t*CH, min((t+1)*CH, total)).
 //    Runs of one bucket that lie entirely inside the chunk are written straight to
 //    buckets[b]; a run that crosses the chunk boundary (the chunk's first and/or last run)
 //    becomes a "partial item" (key b, XYZZ sum) in slot 2t / 2t+1 of the item arrays.
 //    Item slots that stay empty carry key = nb (dropped by the compaction).
+//
+//    The next entry's point is gathered straight into LDS by global_load_lds (16 B per lane
+//    per instruction, lane-linear image [chunk][lane][16 B] per wave) while the current
+//    mixed add runs, so the prefetch costs no VGPRs (the 254-bit madd fits 4 waves per SIMD;
+//    the 381-bit one stays at 2: forced to 3 it spills ~56 VGPRs inside the loop, measured
+//    3.12 vs 2.56 ms at 2^20).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+template <class F>
+struct AccumOcc {  // minimum waves per SIMD k_accum is compiled for
+  static constexpr int waves = F::N >= 28 ? 1 : (F::N >= 14 ? 2 : 4);
+};
+
 template <class C>
-__global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ points,
-                                               const uint32_t *__restrict__ list,
-                                               const uint32_t *__restrict__ offsets, uint32_t nb,
-                                               int CH, uint32_t W, uint32_t B, uint32_t *__restrict__ buckets,
-                                               uint32_t *__restrict__ ikeys, uint32_t *__restrict__ ivals,
-                                               uint32_t nslots) {
+__global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
+    k_accum(const uint32_t *__restrict__ points, const uint32_t *__restrict__ list,
+            const uint32_t *__restrict__ offsets, uint32_t nb, int CH, uint32_t W, uint32_t B,
+            uint32_t *__restrict__ buckets, uint32_t *__restrict__ ikeys, uint32_t *__restrict__ ivals,
+            uint32_t nslots) {
   using F = typename C::Fp;
+  constexpr int AW = aff_words<F>();  // u32 per internal-form point (multiple of 8)
+  constexpr int NCH = AW / 4;         // 16-B chunks per point
+  __shared__ uint4 stage[4][NCH][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (2 * t >= nslots) return;
   const uint32_t total = offsets[nb];
   const uint32_t cs = t * (uint32_t)CH;
+  const bool active = 2 * t < nslots && cs < total;
   uint32_t k0 = nb, k1 = nb;  // item keys of slots 2t, 2t+1
-  if (cs < total) {
+  // gathers the point of list entry `c` (index | sign) into this lane's LDS image
+  auto prefetch = [&](uint32_t c) {
+    const uint32_t *src = points + (size_t)(c & 0x7fffffffu) * AW;
+#pragma unroll
+    for (int j = 0; j < NCH; j++)
+      __builtin_amdgcn_global_load_lds((glb_void_t *)(src + 4 * j), (lds_void_t *)&stage[wave][j][0], 16, 0, 0);
+  };
+  auto read_point = [&](Aff<F> &P) {
+    uint32_t w[AW];
+#pragma unroll
+    for (int j = 0; j < NCH; j++) {
+      const uint4 v = stage[wave][j][lane];
+      w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < F::N; i++) {
+      P.x.v[i] = w[i];
+      P.y.v[i] = w[F::SN + i];
+    }
+  };
+  if (active) {
     const uint32_t ce = min(total, cs + (uint32_t)CH);
     uint32_t b = bucket_of(offsets, nb, cs);
     uint32_t bbeg = offsets[b], bend = offsets[b + 1];
@@ -196,23 +280,24 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
     // consumer (xyzz_add / xyzz_dbl / k_export) takes X and Y only into products, which
     // accept those values.  A settle here would cost two products per flush, paid by the
     // whole wavefront whenever any lane flushes (runs average 32 entries at 2^20).
-    // software pipeline: the point gather for entry e+1 and the list index of entry e+2
-    // are in flight while the madd of entry e runs (clamped to the chunk's last entry, so
-    // every load is in bounds and branch-free); infinity test and negation happen at use
+    // Pipeline: the point of entry e+1 lands in LDS and the list index of entry e+2 in a
+    // register while the madd of entry e runs (clamped to the chunk's last entry, so every
+    // load is in bounds); infinity test and negation happen at use.
     const uint32_t last = ce - 1;
     uint32_t c0 = list[cs], c1 = list[min(cs + 1, last)];
-    Aff<F> P;
-    aff_load(P, points + (size_t)(c0 & 0x7fffffffu) * aff_words<F>());
+    prefetch(c0);
     for (uint32_t e = cs; e < ce; e++) {
-      Aff<F> Pn;
-      aff_load(Pn, points + (size_t)(c1 & 0x7fffffffu) * aff_words<F>());
+      Aff<F> P;
+      read_point(P);  // waits for the gather of entry e
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS image read out before it is refilled
+      prefetch(c1);
       const uint32_t c2 = list[min(e + 2, last)];
       if (e >= bend) {  // run of bucket b ends inside the chunk
         if (first_run && bbeg < cs) {
           xyzz_store(ivals + (size_t)(2 * t) * xyzz_words<F>(), acc);
           k0 = b;
         } else {
-          xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
+          xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
         }
         first_run = false;
         xyzz_set_inf(acc);
@@ -231,7 +316,6 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
         }
         xyzz_acc_aff(acc, P);
       }
-      P = Pn;
       c0 = c1;
       c1 = c2;
     }
@@ -241,11 +325,14 @@ __global__ void __launch_bounds__(256) k_accum(const uint32_t *__restrict__ poin
       xyzz_store(ivals + (size_t)slot * xyzz_words<F>(), acc);
       if (first_run) k0 = b; else k1 = b;
     } else {
-      xyzz_store(buckets + (size_t)bucket_slot(b, W, B) * xyzz_words<F>(), acc);
+      xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (clamped, unused) gather has landed
   }
-  ikeys[2 * t] = k0;
-  ikeys[2 * t + 1] = k1;
+  if (2 * t < nslots) {
+    ikeys[2 * t] = k0;
+    ikeys[2 * t + 1] = k1;
+  }
 }
 
 // 5a. compaction of the partial items (keys < nb), order preserving: scatter by a
@@ -315,7 +402,7 @@ __global__ void __launch_bounds__(BS) k_stitch_blk(const uint32_t *__restrict__ 
   const bool cont_in = touches_start && base > 0 && keys[base - 1] == key;
   const bool cont_out = touches_end && base + nv < M && keys[base + nv] == key;
   if (!cont_in && !cont_out) {
-    xyzz_store(buckets + (size_t)bucket_slot(key, W, B) * XW, acc);
+    xyzz_store(buckets + (size_t)key * XW, acc);
   } else {
     xyzz_store(ovals + (size_t)(touches_start ? 2 * blk : 2 * blk + 1) * XW, acc);
   }
@@ -406,7 +493,7 @@ __global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ bucke
     for (int k = 0; k < per; k++) {
       const int s = lane * per + k;
       const uint32_t m = hiY ? ((uint32_t)seg << l0) + s : ((uint32_t)s << l0) + seg;
-      const uint32_t rank = m * (uint32_t)W + (uint32_t)w;
+      const uint32_t rank = (uint32_t)w * B + m;
       if (offsets[rank + 1] > offsets[rank]) {  // empty buckets hold garbage (never written)
         Xyzz<F> bm;
         xyzz_load(bm, buckets + ((size_t)w * B + m) * xyzz_words<F>());
@@ -457,7 +544,7 @@ __global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buck
   Xyzz<F> acc;
   xyzz_set_inf(acc);
   uint32_t m = bucket_m(part * per);
-  uint32_t rank = m * (uint32_t)W + (uint32_t)w;
+  uint32_t rank = (uint32_t)w * B + m;
   uint32_t o0 = offsets[rank], o1 = offsets[rank + 1];
   Xyzz<F> nxt;
   if (PF) xyzz_load(nxt, wb + (size_t)m * XW);
@@ -468,7 +555,7 @@ __global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buck
     if (PF) cur = nxt;
     if (k + 1 < per) {
       m = bucket_m(part * per + k + 1);
-      rank = m * (uint32_t)W + (uint32_t)w;
+      rank = (uint32_t)w * B + m;
       o0 = offsets[rank];
       o1 = offsets[rank + 1];
       if (PF) xyzz_load(nxt, wb + (size_t)m * XW);
@@ -720,6 +807,11 @@ constexpr int stitch_bs() { return xyzz_words<F>() > 64 ? 128 : 256; }
 static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.n + s.CH - 1) / s.CH); }
 static size_t stitch_slots1(const MsmShape &s, int bs) { return 2 * ((stitch_slots0(s) + bs - 1) / bs) + 2; }
 
+// bucket sort: LDS counting sort up to c = 16 (one window's histogram, 4 B per bucket,
+// fits LDS), hipCUB radix sort beyond
+constexpr int MSM_LDS_SORT_MAX_C = 16;
+static int bits_for(size_t v) { int b = 1; while (((size_t)1 << b) <= v) b++; return b; }
+
 // sorted entries of one pipeline pass: hipCUB takes int counts, offsets are u32
 constexpr size_t MSM_MAX_GROUP_ENTRIES = (size_t)1 << 30;
 // test hook (zkg_msm_set_group_limit): a smaller cap, so tests reach the multi-group path
@@ -738,13 +830,17 @@ static size_t group_bytes(const MsmShape &s) {
   const size_t maxent = (size_t)s.W * s.n;
   const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s, stitch_bs<F>());
   size_t cub = 0, cub2 = 0;
-  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                              (uint32_t *)nullptr, (uint32_t *)nullptr, (int)maxent, 0, s.c));
+  if (s.c <= MSM_LDS_SORT_MAX_C)
+    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(nb + 1)));
+  else
+    ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                (uint32_t *)nullptr, (uint32_t *)nullptr, (int)maxent, 0,
+                                                bits_for(nb)));
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)ns0));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-  add(maxent * 4 * 4);                    // keys, vals, sorted keys, sorted vals
-  add((nb + 1) * 4);                      // offsets
+  add(maxent * 4 * (s.c <= MSM_LDS_SORT_MAX_C ? 2 : 4));  // list, digits (+ radix sort pairs)
+  add((nb + 1) * 4 * 2);                  // counts / slot cursors, offsets
   add(ns0 * (xw + 4) + ns0 * 16 + 64);    // level-0 items, compacted keys + index, flags, pos, count
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
@@ -812,10 +908,12 @@ static void msm_group(Device &dev, const MsmShape &s, const ScalarSlice &sc, int
   hipStream_t st = dev.stream;
   const size_t maxent = (size_t)s.W * n;
   ZK_REQUIRE(maxent <= MSM_MAX_GROUP_ENTRIES, "msm: window group exceeds the sort capacity (internal sizing bug)");
-  uint32_t *keys = dev.arena.take<uint32_t>(maxent);
-  uint32_t *vals = dev.arena.take<uint32_t>(maxent);
-  uint32_t *skeys = dev.arena.take<uint32_t>(maxent);
-  uint32_t *list = dev.arena.take<uint32_t>(maxent);  // sorted values
+  const bool lds_sort = c <= MSM_LDS_SORT_MAX_C;
+  uint32_t *list = dev.arena.take<uint32_t>(maxent);  // bucket-ordered (point index | sign)
+  uint32_t *dig = dev.arena.take<uint32_t>(maxent);   // digits (LDS sort) / ranks (radix sort)
+  uint32_t *vals = lds_sort ? nullptr : dev.arena.take<uint32_t>(maxent);
+  uint32_t *skeys = lds_sort ? nullptr : dev.arena.take<uint32_t>(maxent);
+  uint32_t *counts = dev.arena.take<uint32_t>(nb + 1);
   uint32_t *offsets = dev.arena.take<uint32_t>(nb + 1);
   constexpr int STITCH_BS = stitch_bs<F>();
   const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s, STITCH_BS);
@@ -835,22 +933,48 @@ static void msm_group(Device &dev, const MsmShape &s, const ScalarSlice &sc, int
   uint32_t *P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * xw);
   uint64_t *exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
   size_t cub = 0, cub2 = 0;
-  const int kbits = c;  // in-window digit bits only (see step 2)
-  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
+  const int kbits = bits_for(nb);  // radix sort: ranks < nb, zero digits nb
+  if (lds_sort)
+    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, counts, offsets, (int)(nb + 1), st));
+  else
+    ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, dig, skeys, vals, list, (int)maxent, 0, kbits, st));
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
   if (cub2 > cub) cub = cub2;
   void *cubtmp = dev.arena.take<char>(cub);
 
-  hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff, sc.nread,
-                     sc.mont ? 1 : 0, c, wbase, s.W, keys, vals);
-  ZK_CHECK(hipGetLastError());
-  prof.mark("digits");
-  ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cub, keys, skeys, vals, list, (int)maxent, 0, kbits, st));
+  if (lds_sort) {
+    hipLaunchKernelGGL((k_digits<C, false>), dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff,
+                       sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig, (uint32_t *)nullptr);
+    ZK_CHECK(hipGetLastError());
+    prof.mark("digits");
+    // M entries per workgroup: at least B (so each workgroup's B bucket atomics stay below
+    // its entry count) and enough workgroups to cover the CUs
+    int M = (int)std::max<size_t>((size_t)s.B, ((size_t)n * s.W + 511) / 512);
+    M = (M + 1023) & ~1023;
+    const dim3 grid(div_up(n, M), s.W);
+    const size_t lds = (size_t)s.B * 4;
+    ZK_CHECK(hipFuncSetAttribute((const void *)k_bucket_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    ZK_CHECK(hipFuncSetAttribute((const void *)k_bucket_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    ZK_CHECK(hipMemsetAsync(counts, 0, (nb + 1) * 4, st));
+    hipLaunchKernelGGL(k_bucket_lds<false>, grid, dim3(1024), lds, st, dig, n, M, c, counts, (uint32_t *)nullptr);
+    ZK_CHECK(hipGetLastError());
+    size_t cb = cub;
+    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, counts, offsets, (int)(nb + 1), st));
+    ZK_CHECK(hipMemcpyAsync(counts, offsets, nb * 4, hipMemcpyDeviceToDevice, st));  // slot cursors
+    hipLaunchKernelGGL(k_bucket_lds<true>, grid, dim3(1024), lds, st, dig, n, M, c, counts, list);
+    ZK_CHECK(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL((k_digits<C, true>), dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff,
+                       sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig, vals);
+    ZK_CHECK(hipGetLastError());
+    prof.mark("digits");
+    size_t cb = cub;
+    ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cb, dig, skeys, vals, list, (int)maxent, 0, kbits, st));
+    hipLaunchKernelGGL(k_offsets_scan, dim3(div_up(maxent, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
+                       (uint32_t)nb, offsets);
+    ZK_CHECK(hipGetLastError());
+  }
   prof.mark("sort");
-  hipLaunchKernelGGL(k_offsets_scan, dim3(div_up(maxent, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
-                     (uint32_t)nb, c, (uint32_t)s.W, offsets);
-  ZK_CHECK(hipGetLastError());
-  prof.mark("offsets");
   const bool timed = wbase == 0;
   if (timed) timer_begin(dev);
   // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
@@ -1012,8 +1136,8 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   if (host_inputs) {
     uint64_t *a = dev.arena.take<uint64_t>((size_t)n * sc_in.stride);
     uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
-    ZK_CHECK(hipMemcpyAsync(a, sc_in.data, sc_bytes, hipMemcpyHostToDevice, st));
-    ZK_CHECK(hipMemcpyAsync(b, points, pt_bytes, hipMemcpyHostToDevice, st));
+    copy_h2d_staged(dev, a, sc_in.data, sc_bytes);
+    copy_h2d_staged(dev, b, points, pt_bytes);
     sc.data = a;
     d_pt = b;
   }

@@ -366,16 +366,29 @@ def end_to_end(zk, curve, scalars, points, device_ms, ntt, args, reps=5):
         m = args.ntt_log
         x = zk.gen_fr("bls12_381", 0x5A4B0003, 1 << m)
         sg = zk.get_fft_subgroup("bls12_381", m)
-        for name, fn, key in (("ntt_forward", zk.forward_ntt, "forward"), ("ntt_inverse", zk.inverse_ntt, "inverse")):
+        lib = zk.load()
+        reused = np.zeros_like(x)
+        reused.fill(1)  # pages resident
+        g = sg.gen_array()
+        for name, key in (("ntt_forward", "forward"), ("ntt_inverse", "inverse")):
+            sym = getattr(lib, f"bls12_381_poly_mont_{name}")
+            fn = zk.forward_ntt if key == "forward" else zk.inverse_ntt
             fn(sg, x)
             t0 = time.perf_counter()
             for _ in range(2):
-                y = fn(sg, x)
+                y = fn(sg, x)  # fresh output array per call, as the Haskell binding allocates
             dt = (time.perf_counter() - t0) / 2
+            t0 = time.perf_counter()
+            for _ in range(2):
+                sym(m, zk._p(g), zk._p(x), zk._p(reused))
+            dt2 = (time.perf_counter() - t0) / 2
             dev = ntt[key]["ms"]
             out[name] = {"symbol": f"bls12_381_poly_mont_{name}", "elems_per_s": x.shape[0] / dt, "ms": dt * 1e3,
+                         "ms_reused_output": dt2 * 1e3, "elems_per_s_reused_output": x.shape[0] / dt2,
                          "device_resident_ms": dev, "pcie_bytes": 2 * x.nbytes,
-                         "pcie_GBps_effective": 2 * x.nbytes / max(dt - dev * 1e-3, 1e-9) / 1e9}
+                         "pcie_GBps_effective": 2 * x.nbytes / max(dt2 - dev * 1e-3, 1e-9) / 1e9,
+                         "note": "ms: fresh numpy output per call (first touch of 512 MiB of new pages is paid "
+                                 "inside the call); ms_reused_output: the same symbol into a resident buffer"}
         del y
     return out
 

@@ -1,3 +1,3 @@
 # scratch commands of the current GPU experiment (run by tools/gpu_job.sh step "cmd")
 set -e
-timeout 120 tools/microbench/copy_bw
+python bench.py --steps 3 --no-cpu-baseline --ntt-steps 2

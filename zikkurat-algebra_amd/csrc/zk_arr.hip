@@ -414,12 +414,12 @@ struct Stage {
   const uint64_t *in(const uint64_t *p, size_t n) {
     if (!host || !p) return p;
     uint64_t *d = dev.arena.take<uint64_t>(n * 4);
-    copy_h2d_staged(dev, d, p, n * 32);
+    if (n) ZK_CHECK(hipMemcpyAsync(d, p, n * 32, hipMemcpyHostToDevice, dev.stream));
     return d;
   }
   uint64_t *out(uint64_t *p, size_t n) { return host ? dev.arena.take<uint64_t>(n * 4) : p; }
   void back(uint64_t *host_p, const uint64_t *dev_p, size_t n) {
-    if (host && n) copy_d2h_staged(dev, host_p, dev_p, n * 32);
+    if (host && n) ZK_CHECK(hipMemcpyAsync(host_p, dev_p, n * 32, hipMemcpyDeviceToHost, dev.stream));
   }
 };
 

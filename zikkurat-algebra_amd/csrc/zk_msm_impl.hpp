@@ -1136,8 +1136,11 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   if (host_inputs) {
     uint64_t *a = dev.arena.take<uint64_t>((size_t)n * sc_in.stride);
     uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
-    copy_h2d_staged(dev, a, sc_in.data, sc_bytes);
-    copy_h2d_staged(dev, b, points, pt_bytes);
+    // caller memory is pageable; the runtime's pageable path runs at PCIe rate on MI355X
+    // hosts (56 GB/s measured, tools/microbench/copy_bw.hip), a pinned bounce buffer only
+    // adds a host copy
+    ZK_CHECK(hipMemcpyAsync(a, sc_in.data, sc_bytes, hipMemcpyHostToDevice, st));
+    ZK_CHECK(hipMemcpyAsync(b, points, pt_bytes, hipMemcpyHostToDevice, st));
     sc.data = a;
     d_pt = b;
   }

@@ -509,7 +509,7 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   uint64_t *d_dst = dst;
   if (host_io) {
     uint64_t *a = dev.arena.take<uint64_t>(N * F::N64);
-    copy_h2d_staged(dev, a, src, N * elbytes);
+    ZK_CHECK(hipMemcpyAsync(a, src, N * elbytes, hipMemcpyHostToDevice, st));
     d_src = a;
     d_dst = dev.arena.take<uint64_t>(N * F::N64);
   }
@@ -553,7 +553,7 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     in = out;
     T <<= r;
   }
-  if (host_io) copy_d2h_staged(dev, dst, d_dst, N * elbytes);
+  if (host_io) ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
   ZK_CHECK(hipStreamSynchronize(st));
   timer_collect(dev);
 }

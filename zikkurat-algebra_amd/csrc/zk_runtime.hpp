@@ -74,23 +74,10 @@ struct Device {
   size_t pinned_cap = 0;
   void *host_staging(size_t bytes);
   KernelTimer timer;
-  // pinned ring for staging caller (pageable) memory, see copy_h2d_staged
-  void *ring[2] = {nullptr, nullptr};
-  hipEvent_t ring_ev[2] = {nullptr, nullptr};
 };
 
 // The device of the calling thread (hipGetDevice), lazily initialised.
 Device &current_device();
-
-// Copies between CALLER memory (ordinary pageable host memory, as GHC's pinned ForeignPtrs
-// are to the OS) and device memory on dev.stream, through a ring of two pinned 32 MiB
-// chunks: the host thread pool copies chunk k into one pinned chunk while the DMA engine
-// moves chunk k-1 from the other, so both run at full speed and overlap (pageable
-// hipMemcpy stages through the driver serially: ~15-20 GB/s D2H measured).  Caller holds
-// dev.mu.  copy_h2d_staged returns with the copies enqueued (the pinned chunks are reused
-// only after their DMA completed); copy_d2h_staged returns when dst holds the data.
-void copy_h2d_staged(Device &dev, void *dst_dev, const void *src_host, size_t bytes);
-void copy_d2h_staged(Device &dev, void *dst_host, const void *src_dev, size_t bytes);
 
 // kernel timer (caller holds dev.mu for begin/end/collect)
 void timer_set_enabled(bool on);

@@ -39,7 +39,11 @@ def run(curve, logn, windows, reps=5, profile=False):
 
 
 if __name__ == "__main__":
-    if sys.argv[1] == "phases":
+    if sys.argv[1] == "phases2":  # last phase line + the timing line per size
+        import contextlib, io
+        for curve, logn in (("bls12_381", 20), ("bls12_381", 16), ("bn128", 20)):
+            run(curve, logn, [0], reps=4, profile=True)
+    elif sys.argv[1] == "phases":
         for curve, logn in (("bls12_381", 20), ("bn128", 20), ("bls12_381", 16), ("bls12_381", 14),
                             ("bls12_381", 23)):
             run(curve, logn, [0], reps=4, profile=True)

@@ -761,8 +761,9 @@ struct MsmShape {
 static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; return r; }
 
 // Shape of one pipeline pass over W windows of n scalars.  The constants were swept on
-// MI355X (round 1, profiles/r01_*): Y sums take 16 buckets per lane at scale, the weighted
-// job sums 8 items per lane, the accumulation 64 sorted entries per lane (128 from 2^25
+// MI355X (profiles/r01_*, profiles/r02h_qy_qa_sweep.txt): Y sums take 16 buckets per lane at
+// scale (8: ysum 0.37 -> 0.48 ms, 4: 0.66 ms at BLS12-381 2^20), the weighted job sums 8
+// items per lane (4: no change), the accumulation 64 sorted entries per lane (128 from 2^25
 // entries on, profiles/r01_v7_ch_sweep.txt).
 static MsmShape make_shape(int n, int c, int W) {
   MsmShape s;

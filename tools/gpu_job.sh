@@ -10,6 +10,7 @@
 #   pmcf      rocprofv3 --pmc FETCH_SIZE (own pass) -> gpurun_out/TAG_pmcf/
 #   pmcw      rocprofv3 --pmc WRITE_SIZE (own pass) -> gpurun_out/TAG_pmcw/
 #   pmcsq     rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU ... (VALU issue, own pass) -> gpurun_out/TAG_pmcsq/
+#   calib     rocprofv3 --pmc FETCH_SIZE of tools/microbench/gather_calib (known bytes) -> gpurun_out/TAG_calib/
 #   listpmc   rocprofv3 -L (available counters)   -> gpurun_out/TAG_counters.txt
 #   ceiling   tools/microbench/valu_ceiling (prebuilt) -> gpurun_out/TAG_ceiling.json
 #   ext       tools/bench_ext.py                  -> gpurun_out/TAG_ext.json
@@ -38,6 +39,8 @@ for step in "$@"; do
               > /dev/null 2> ${O}_pmcw.err ;;
     pmcsq) timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
               -d ${O}_pmcsq -o run --output-format csv -- python3 $BENCH_SHORT > /dev/null 2> ${O}_pmcsq.err ;;
+    calib) timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d ${O}_calib -o run --output-format csv -- tools/microbench/gather_calib \
+              > ${O}_calib.log 2>&1 ;;
     listpmc) timeout -k 10 120 rocprofv3 -L > ${O}_counters.txt 2>&1 ;;
     ceiling) timeout -k 10 120 tools/microbench/valu_ceiling > ${O}_ceiling.json 2> ${O}_ceiling.err ;;
     ext) timeout -k 10 400 python -u tools/bench_ext.py > ${O}_ext.json 2> ${O}_ext.err ;;

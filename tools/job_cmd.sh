@@ -1,7 +1,8 @@
 # scratch commands of the current GPU experiment (run by tools/gpu_job.sh step "cmd")
 set -e
-timeout 100 python tools/sweep_window.py bls12_381 14 6 7 8 9 10 11 12
-timeout 100 python tools/sweep_window.py bls12_381 16 8 9 10 11 12 13 14
-timeout 100 python tools/sweep_window.py bls12_381 18 11 12 13 14 15 16
-timeout 100 python tools/sweep_window.py bn128 16 8 9 10 11 12 13 14
-timeout 100 python tools/sweep_window.py bls12_381 12 5 6 7 8 9 10
+for v in base chain base chain; do
+  if [ $v = base ]; then export ZK_LIB_PATH=; else export ZK_LIB_PATH=$PWD/variants/$v/libzkalgebra_gpu.so; fi
+  echo "== $v"
+  timeout 100 python tools/sweep_window.py bls12_381 20
+  timeout 100 python tools/sweep_window.py bn128 20
+done

@@ -330,6 +330,29 @@ __device__ __forceinline__ void fe_canon(Fe<F> &a) {
   for (int i = 0; i < F::N; i++) a.v[i] = lt ? a.v[i] : d[i];
 }
 
+// normalised limbs holding a value v < 64p (< 2^261 for the 9 x 29-bit fields) -> same
+// residue, < 2p, without a product: q = floor(v / p) is estimated from the top limb with a
+// reciprocal of p's top 64 bits (q_est = q or q - 1), then v - q_est p.  ~40 VALU ops
+// instead of a Montgomery product by one (the NTT's last-pass closing step).
+template <class F>
+__host__ __device__ constexpr uint64_t fe_qk() {  // floor(2^64 / (floor(p / 2^(RB (N-1) - 32)) + 1))
+  static_assert(F::N == 9 && F::RB == 29, "derived for the 9 x 29-bit fields");
+  // p / 2^200 from limbs 6 (bits 174..202), 7 (203..231), 8 (232..260)
+  return ~0ull / ((((uint64_t)F::p(8) << 32) | ((uint64_t)F::p(7) << 3) | (F::p(6) >> 26)) + 1);
+}
+template <class F>
+__device__ __forceinline__ void fe_reduce_small(Fe<F> &v) {
+  constexpr uint64_t K = fe_qk<F>();
+  const uint32_t q = (uint32_t)(((uint64_t)v.v[F::N - 1] * K) >> 32);
+  int64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {
+    const int64_t t = (int64_t)v.v[i] - (int64_t)((uint64_t)q * F::p(i)) + carry;
+    v.v[i] = (i < F::N - 1) ? ((uint32_t)t & F::MASK) : (uint32_t)t;
+    carry = t >> F::RB;
+  }
+}
+
 // any value < (R'/2) (normalised or lazily grown limbs < 2^31) -> same residue, < 2p
 template <class F>
 __device__ __forceinline__ void fe_reduce(Fe<F> &a) {

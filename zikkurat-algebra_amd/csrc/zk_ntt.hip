@@ -114,6 +114,17 @@ __global__ void k_tw_inner_int(uint32_t *__restrict__ itw_i, const uint64_t *__r
 
 // ---------------------------------------------------------------------------- pass kernel
 
+// LDS slot of tile element I: an XOR swizzle of the low 6 index bits by bits 6..9, so that
+// every access pattern of the pass (bit-reversed loads, the radix-4 rounds at every stride,
+// G-interleaved stores) hits 64 distinct banks with 9-word elements (verified by brute
+// force over the tile shapes; the plain layout had 4-16-way conflicts: rocprofv3
+// SQ_LDS_BANK_CONFLICT was 80 % of the LDS-active cycles, profiles/r02o_ntt_lds.txt)
+__device__ __forceinline__ uint32_t lds_slot(uint32_t I) {
+  const uint32_t m1 = (I >> 6) & 3, m2 = (I >> 8) & 3;
+  const uint32_t x = m1 ^ m2;
+  return I ^ (m1 | (x << 2) | (x << 4));
+}
+
 template <class F>
 __device__ __forceinline__ void lds_get(Fe<F> &x, const uint32_t *p) {
 #pragma unroll
@@ -146,10 +157,10 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
       const int g = u / q4, j = u % q4;
       const int i0 = g * R + j * 4;
       Fe<F> a0, a1, a2, a3, b0, b1, b3, t;
-      lds_get(a0, data + (size_t)i0 * NW);
-      lds_get(a1, data + (size_t)(i0 + 1) * NW);
-      lds_get(a2, data + (size_t)(i0 + 2) * NW);
-      lds_get(a3, data + (size_t)(i0 + 3) * NW);
+      lds_get(a0, data + (size_t)lds_slot(i0) * NW);
+      lds_get(a1, data + (size_t)lds_slot(i0 + 1) * NW);
+      lds_get(a2, data + (size_t)lds_slot(i0 + 2) * NW);
+      lds_get(a3, data + (size_t)lds_slot(i0 + 3) * NW);
       fe_add_lazy(b0, a0, a1);
       fe_sub_lazy(b1, a0, a1);
       fe_sub_lazy(b3, a2, a3);
@@ -164,10 +175,10 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
       fe_norm(a1);
       fe_norm(a2);
       fe_norm(a3);
-      lds_put(data + (size_t)i0 * NW, a0);
-      lds_put(data + (size_t)(i0 + 1) * NW, a1);
-      lds_put(data + (size_t)(i0 + 2) * NW, a2);
-      lds_put(data + (size_t)(i0 + 3) * NW, a3);
+      lds_put(data + (size_t)lds_slot(i0) * NW, a0);
+      lds_put(data + (size_t)lds_slot(i0 + 1) * NW, a1);
+      lds_put(data + (size_t)lds_slot(i0 + 2) * NW, a2);
+      lds_put(data + (size_t)lds_slot(i0 + 3) * NW, a3);
     }
     __syncthreads();
     s = 2;
@@ -180,10 +191,10 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
       const int blk = j >> s, off = j & (half - 1);
       const int i0 = g * R + blk * 4 * half + off;
       Fe<F> a0, a1, a2, a3, w1, w2, w3, t;
-      lds_get(a0, data + (size_t)i0 * NW);
-      lds_get(a1, data + (size_t)(i0 + half) * NW);
-      lds_get(a2, data + (size_t)(i0 + 2 * half) * NW);
-      lds_get(a3, data + (size_t)(i0 + 3 * half) * NW);
+      lds_get(a0, data + (size_t)lds_slot(i0) * NW);
+      lds_get(a1, data + (size_t)lds_slot(i0 + half) * NW);
+      lds_get(a2, data + (size_t)lds_slot(i0 + 2 * half) * NW);
+      lds_get(a3, data + (size_t)lds_slot(i0 + 3 * half) * NW);
       lds_get(w1, itw + (size_t)(off * (R / (2 * half))) * ITW_STRIDE);           // w_{2h}^off
       lds_get(w2, itw + (size_t)(off * (R / (4 * half))) * ITW_STRIDE);           // w_{4h}^off
       lds_get(w3, itw + (size_t)((off + half) * (R / (4 * half))) * ITW_STRIDE);  // w_{4h}^(off+h)
@@ -206,10 +217,10 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
       fe_norm(a1);
       fe_norm(a2);
       fe_norm(a3);
-      lds_put(data + (size_t)i0 * NW, a0);
-      lds_put(data + (size_t)(i0 + half) * NW, a1);
-      lds_put(data + (size_t)(i0 + 2 * half) * NW, a2);
-      lds_put(data + (size_t)(i0 + 3 * half) * NW, a3);
+      lds_put(data + (size_t)lds_slot(i0) * NW, a0);
+      lds_put(data + (size_t)lds_slot(i0 + half) * NW, a1);
+      lds_put(data + (size_t)lds_slot(i0 + 2 * half) * NW, a2);
+      lds_put(data + (size_t)lds_slot(i0 + 3 * half) * NW, a3);
     }
     __syncthreads();
   }
@@ -221,16 +232,16 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
       const int blk = j >> s, off = j & (half - 1);
       const int i0 = g * R + blk * 2 * half + off;
       Fe<F> a, b, w, t, x, y;
-      lds_get(a, data + (size_t)i0 * NW);
-      lds_get(b, data + (size_t)(i0 + half) * NW);
+      lds_get(a, data + (size_t)lds_slot(i0) * NW);
+      lds_get(b, data + (size_t)lds_slot(i0 + half) * NW);
       lds_get(w, itw + (size_t)(off * (R / (2 * half))) * ITW_STRIDE);
       fe_mul(t, b, w);
       fe_add_lazy(x, a, t);
       fe_sub_lazy(y, a, t);
       fe_norm(x);
       fe_norm(y);
-      lds_put(data + (size_t)i0 * NW, x);
-      lds_put(data + (size_t)(i0 + half) * NW, y);
+      lds_put(data + (size_t)lds_slot(i0) * NW, x);
+      lds_put(data + (size_t)lds_slot(i0 + half) * NW, y);
     }
     __syncthreads();
   }
@@ -238,8 +249,19 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
 
 struct PassArgs {
   int m, r, S, T, last, G, P;
+  int h;    // split of the two-level power tables (tlo: 2^h entries)
+  int otf;  // non-last pass: inter-pass twiddles computed from tlo/thi instead of a table
   int dig[8];  // log2 radix of every pass
 };
+
+// Inter-pass twiddle tables hold R_p * S_p entries (32 B each); a pass whose table would
+// exceed 2^25 entries (1 GiB) computes its twiddles on the fly from the two-level tables
+// (one more product per element) instead.  At 2^24 pass 0's table is the whole
+// transform's size (512 MiB) and still pays: the pass is VALU-bound, and computing the
+// twiddles measured 0.08 ms slower per transform than streaming them (profiles/r02p_*).
+#ifndef ZK_NTT_TABLE_MAX
+#define ZK_NTT_TABLE_MAX ((size_t)1 << 25)
+#endif
 
 // One pass.  Block = one tile of G instances x R elements.
 //   non-last pass: instance (hi, lo), lo in [0, S); element k at hi*R*S + k*S + lo
@@ -250,7 +272,9 @@ template <class F>
 __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__restrict__ src, uint64_t *__restrict__ dst,
                                                           PassArgs a, const uint32_t *__restrict__ itw_i,
                                                           const uint64_t *__restrict__ tab,
-                                                          const uint64_t *__restrict__ scale) {
+                                                          const uint64_t *__restrict__ scale,
+                                                          const uint64_t *__restrict__ tlo,
+                                                          const uint64_t *__restrict__ thi) {
   extern __shared__ uint32_t lds[];
   constexpr int NW = F::N;
   const int r = a.r, G = a.G, S = a.S;
@@ -306,7 +330,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
     Fe<F> x;
     fe_load_ref(x, src + addr * F::N64);
     const int kr = r ? (int)(__builtin_bitreverse32((uint32_t)k) >> (32 - r)) : 0;
-    lds_put(data + ((size_t)g * R + kr) * NW, x);
+    lds_put(data + (size_t)lds_slot((uint32_t)(g * R + kr)) * NW, x);
   }
   __syncthreads();
 
@@ -323,21 +347,27 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
   for (int e = tid; e < nel; e += NTT_THREADS) {
     const int g = e % G, k = e / G;  // consecutive threads -> consecutive g (coalesced)
     Fe<F> x;
-    lds_get(x, data + ((size_t)g * R + k) * NW);
+    lds_get(x, data + (size_t)lds_slot((uint32_t)(g * R + k)) * NW);
     size_t addr;
     if (!a.last) {
       addr = hi_base + (size_t)k * S + g;
       Fe<F> w, y;
-      fe_load_ref(w, tab + ((size_t)k * S + (addr % S)) * F::N64);
+      if (a.otf) tw2(w, tlo, thi, a.h, (uint32_t)a.T * (uint32_t)k * (uint32_t)(addr % S));
+      else fe_load_ref(w, tab + ((size_t)k * S + (addr % S)) * F::N64);
       fe_mul(y, x, w);
       x = y;
     } else {
       addr = (a.P == 1) ? (size_t)k : nat_base + (size_t)(k0base + g) + (size_t)k * a.T;
-      // closing product: the scale (1/N) or internal one (R' mod p) maps the lazily
-      // grown value (< 33p) back below 2p, as fe_store_ref's canonicalisation needs
-      Fe<F> y;
-      fe_mul(y, x, sc);
-      x = y;
+      // closing step: the lazily grown value (< 34p) back below 2p, as fe_store_ref's
+      // canonicalisation needs -- by the product with the scale (1/N) when an inverse's
+      // scale has no table to ride on, else by a product-free reduction
+      if (scale) {
+        Fe<F> y;
+        fe_mul(y, x, sc);
+        x = y;
+      } else {
+        fe_reduce_small(x);
+      }
     }
     fe_store_ref(dst + addr * F::N64, x);
   }
@@ -360,7 +390,9 @@ struct TwSet {
   std::vector<uint64_t *> inner; // per pass: R_p/2 inner twiddles
   std::vector<uint32_t *> inner_i; // the same, internal limbs, ITW_STRIDE u32 per entry
   std::vector<uint64_t *> tab;   // per non-last pass: R_p * S_p table
-  uint64_t *scale = nullptr;     // 1/N (reference form) for the single-pass inverse
+  uint64_t *scale = nullptr;     // 1/N (reference form) for the last pass of an inverse, unless a table holds it
+  uint64_t *tlo = nullptr, *thi = nullptr;  // two-level power tables (2^h and 2^(m-h) entries)
+  int h = 0;
   size_t bytes = 0;
   uint64_t last_use = 0;
 };
@@ -414,7 +446,10 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
     S >>= dig[p];
     words += ((size_t)1 << dig[p]) / 2 * el + el;
     words += ((size_t)1 << dig[p]) / 2 * (ITW_STRIDE / 2) + 2;
-    if (p < P - 1) { tab_words[p] = ((size_t)1 << dig[p]) * S * el; words += tab_words[p]; }
+    if (p < P - 1 && ((size_t)1 << dig[p]) * S <= ZK_NTT_TABLE_MAX) {
+      tab_words[p] = ((size_t)1 << dig[p]) * S * el;
+      words += tab_words[p];
+    }
     T <<= dig[p];
   }
   // evict least-recently used sets beyond the cache limit
@@ -469,7 +504,7 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
       ZK_CHECK(hipGetLastError());
     }
     ts.inner_i.push_back(inner_i);
-    if (p < P - 1) {
+    if (p < P - 1 && tab_words[p]) {
       uint64_t *tab = take(tab_words[p]);
       const size_t cnt = ((size_t)1 << r) * S;
       hipLaunchKernelGGL(k_tw_pass<F>, dim3(div_up(cnt, 256)), dim3(256), 0, st, tab, 1 << r, (int)S, (uint32_t)T,
@@ -481,7 +516,12 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
     }
     T <<= r;
   }
-  ts.scale = (inverse && P == 1) ? d_ninv : nullptr;
+  // the inverse's 1/N rides on pass 0's table when there is one, else on the last pass's
+  // closing product
+  ts.scale = (inverse && (P == 1 || !tab_words[0])) ? d_ninv : nullptr;
+  ts.tlo = tlo;
+  ts.thi = thi;
+  ts.h = h;
   ts.last_use = ++g_tw_clock;
   return g_tw.emplace(key, ts).first->second;
 }
@@ -544,10 +584,12 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     pa.T = (int)T;
     pa.last = last;
     pa.G = G;
+    pa.h = tw.h;
+    pa.otf = (!last && !tw.tab[p]) ? 1 : 0;
     ZK_CHECK(hipFuncSetAttribute((const void *)k_ntt_pass<F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (p == 0) timer_begin(dev);
     hipLaunchKernelGGL(k_ntt_pass<F>, dim3((unsigned)ntiles), dim3(NTT_THREADS), lds, st, in, out, pa, tw.inner_i[p],
-                       tw.tab[p], last ? tw.scale : nullptr);
+                       tw.tab[p], last ? tw.scale : nullptr, tw.tlo, tw.thi);
     ZK_CHECK(hipGetLastError());
     if (last) timer_end(dev);
     in = out;

@@ -1,6 +1,12 @@
 # scratch commands of the current GPU experiment (run by tools/gpu_job.sh step "cmd")
 set -e
-timeout 200 python -u -m pytest tests/test_gpu_ntt.py tests/test_gpu_g1ext.py tests/test_gpu_arr.py -x -q --timeout 120 --timeout-method thread
-for v in base base; do
-  timeout 100 python bench.py --steps 2 --warmup 1 --no-e2e --no-cpu-baseline --ntt-steps 5 | python -c "import json,sys; d=json.load(sys.stdin)['ntt']; print({k: (d[k]['ms'], d[k]['kernel_ms']) for k in ('forward','inverse')}, d['parity_vs_reference'])"
+timeout 300 python -u -m pytest tests/test_gpu_msm.py tests/test_gpu_concurrency.py -x -q --timeout 120 --timeout-method thread
+for v in base nopipe pipe14 base nopipe; do
+  if [ $v = base ]; then export ZK_LIB_PATH=; else export ZK_LIB_PATH=$PWD/variants/$v/libzkalgebra_gpu.so; fi
+  echo "== $v"
+  timeout 100 python tools/sweep_window.py bls12_381 20
+  timeout 100 python tools/sweep_window.py bn128 20
+  timeout 100 python tools/sweep_window.py bls12_381 16
+  timeout 100 python tools/sweep_window.py bls12_381 18
+  timeout 100 python tools/sweep_window.py bls12_381 14
 done

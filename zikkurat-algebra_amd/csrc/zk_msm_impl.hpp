@@ -898,97 +898,137 @@ struct ScalarSlice {
 
 // One pass of the device pipeline over windows [wbase, wbase + s.W): digits, bucket sort,
 // accumulation, stitch, Y sums, job sums, export; the (window, job) sums land in the pinned
-// host buffer h (reference-form XYZZ, window-major).  Synchronises the stream.
+// host buffer h (reference-form XYZZ, window-major).  launch() enqueues everything on the
+// pass's stream without a host round trip; finish() synchronises it and, only for skewed
+// scalars whose partial runs need more than the speculative stitch levels, runs the rest.
 template <class C>
-static void msm_group(Device &dev, const MsmShape &s, const ScalarSlice &sc, int wbase, const uint32_t *pts_int,
-                      uint64_t *h, uint32_t *hc, PhaseProf &prof) {
+struct GroupPass {
   using F = typename C::Fp;
-  const int n = s.n, c = s.c;
-  const size_t nb = (size_t)s.W * s.B;
-  const size_t xw = xyzz_words<F>();
-  hipStream_t st = dev.stream;
-  const size_t maxent = (size_t)s.W * n;
-  ZK_REQUIRE(maxent <= MSM_MAX_GROUP_ENTRIES, "msm: window group exceeds the sort capacity (internal sizing bug)");
-  const bool lds_sort = c <= MSM_LDS_SORT_MAX_C;
-  uint32_t *list = dev.arena.take<uint32_t>(maxent);  // bucket-ordered (point index | sign)
-  uint32_t *dig = dev.arena.take<uint32_t>(maxent);   // digits (LDS sort) / ranks (radix sort)
-  uint32_t *vals = lds_sort ? nullptr : dev.arena.take<uint32_t>(maxent);
-  uint32_t *skeys = lds_sort ? nullptr : dev.arena.take<uint32_t>(maxent);
-  uint32_t *counts = dev.arena.take<uint32_t>(nb + 1);
-  uint32_t *offsets = dev.arena.take<uint32_t>(nb + 1);
-  constexpr int STITCH_BS = stitch_bs<F>();
-  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s, STITCH_BS);
-  uint32_t *ikeys0 = dev.arena.take<uint32_t>(ns0);
-  uint32_t *ivals0 = dev.arena.take<uint32_t>(ns0 * xw);
-  uint32_t *ckeys = dev.arena.take<uint32_t>(ns0);
-  uint32_t *cidx = dev.arena.take<uint32_t>(ns0);
-  uint32_t *flags = dev.arena.take<uint32_t>(ns0);
-  uint32_t *pos = dev.arena.take<uint32_t>(ns0);
-  uint32_t *ccount = dev.arena.take<uint32_t>(16);
-  uint32_t *okA = dev.arena.take<uint32_t>(ns1);
-  uint32_t *ovA = dev.arena.take<uint32_t>(ns1 * xw);
-  uint32_t *okB = dev.arena.take<uint32_t>(ns1);
-  uint32_t *ovB = dev.arena.take<uint32_t>(ns1 * xw);
-  uint32_t *buckets = dev.arena.take<uint32_t>(nb * xw);
-  uint32_t *Y = dev.arena.take<uint32_t>((size_t)s.W * s.NY * xw);
-  uint32_t *P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * xw);
-  uint64_t *exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
-  size_t cub = 0, cub2 = 0;
-  const int kbits = bits_for(nb);  // radix sort: ranks < nb, zero digits nb
-  if (lds_sort)
-    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, counts, offsets, (int)(nb + 1), st));
-  else
-    ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, dig, skeys, vals, list, (int)maxent, 0, kbits, st));
-  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
-  if (cub2 > cub) cub = cub2;
-  void *cubtmp = dev.arena.take<char>(cub);
+  static constexpr int STITCH_BS = stitch_bs<F>();
+  Device &dev;
+  MsmShape s;
+  ScalarSlice sc;
+  int wbase, timer_slot;
+  const uint32_t *pts_int;
+  uint64_t *h;
+  uint32_t *hc;
+  PhaseProf *prof;
+  hipStream_t st;
+  size_t nb, xw, maxent, ns0, ns1, cub = 0;
+  bool lds_sort, done = false;
+  uint32_t *list, *dig, *vals, *skeys, *counts, *offsets, *ikeys0, *ivals0, *ckeys, *cidx, *flags, *pos, *ccount;
+  uint32_t *okA, *ovA, *okB, *ovB, *buckets, *Y, *P0;
+  uint64_t *exp;
+  void *cubtmp;
+  // stitch state (level ping-pong)
+  const uint32_t *inK, *inV;
+  size_t slots;
+  uint32_t *outK, *outV, *altK, *altV;
 
-  if (lds_sort) {
-    hipLaunchKernelGGL((k_digits<C, false>), dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff,
-                       sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig, (uint32_t *)nullptr);
-    ZK_CHECK(hipGetLastError());
-    prof.mark("digits");
-    // M entries per workgroup: at least B (so each workgroup's B bucket atomics stay below
-    // its entry count) and enough workgroups to cover the CUs
-    int M = (int)std::max<size_t>((size_t)s.B, ((size_t)n * s.W + 511) / 512);
-    M = (M + 1023) & ~1023;
-    const dim3 grid(div_up(n, M), s.W);
-    const size_t lds = (size_t)s.B * 4;
-    ZK_CHECK(hipFuncSetAttribute((const void *)k_bucket_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    ZK_CHECK(hipFuncSetAttribute((const void *)k_bucket_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    ZK_CHECK(hipMemsetAsync(counts, 0, (nb + 1) * 4, st));
-    hipLaunchKernelGGL(k_bucket_lds<false>, grid, dim3(1024), lds, st, dig, n, M, c, counts, (uint32_t *)nullptr);
-    ZK_CHECK(hipGetLastError());
-    size_t cb = cub;
-    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, counts, offsets, (int)(nb + 1), st));
-    ZK_CHECK(hipMemcpyAsync(counts, offsets, nb * 4, hipMemcpyDeviceToDevice, st));  // slot cursors
-    hipLaunchKernelGGL(k_bucket_lds<true>, grid, dim3(1024), lds, st, dig, n, M, c, counts, list);
-    ZK_CHECK(hipGetLastError());
-  } else {
-    hipLaunchKernelGGL((k_digits<C, true>), dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff,
-                       sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig, vals);
-    ZK_CHECK(hipGetLastError());
-    prof.mark("digits");
-    size_t cb = cub;
-    ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cb, dig, skeys, vals, list, (int)maxent, 0, kbits, st));
-    hipLaunchKernelGGL(k_offsets_scan, dim3(div_up(maxent, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
-                       (uint32_t)nb, offsets);
-    ZK_CHECK(hipGetLastError());
+  GroupPass(Device &d, const MsmShape &shape, const ScalarSlice &scal, int wb, const uint32_t *pts, uint64_t *hh,
+            uint32_t *hcc, PhaseProf *pr, hipStream_t stream, int tslot)
+      : dev(d), s(shape), sc(scal), wbase(wb), timer_slot(tslot), pts_int(pts), h(hh), hc(hcc), prof(pr),
+        st(stream) {
+    const int n = s.n;
+    nb = (size_t)s.W * s.B;
+    xw = xyzz_words<F>();
+    maxent = (size_t)s.W * n;
+    ZK_REQUIRE(maxent <= MSM_MAX_GROUP_ENTRIES, "msm: window group exceeds the sort capacity (internal sizing bug)");
+    lds_sort = s.c <= MSM_LDS_SORT_MAX_C;
+    list = dev.arena.take<uint32_t>(maxent);  // bucket-ordered (point index | sign)
+    dig = dev.arena.take<uint32_t>(maxent);   // digits (LDS sort) / ranks (radix sort)
+    vals = lds_sort ? nullptr : dev.arena.take<uint32_t>(maxent);
+    skeys = lds_sort ? nullptr : dev.arena.take<uint32_t>(maxent);
+    counts = dev.arena.take<uint32_t>(nb + 1);
+    offsets = dev.arena.take<uint32_t>(nb + 1);
+    ns0 = stitch_slots0(s);
+    ns1 = stitch_slots1(s, STITCH_BS);
+    ikeys0 = dev.arena.take<uint32_t>(ns0);
+    ivals0 = dev.arena.take<uint32_t>(ns0 * xw);
+    ckeys = dev.arena.take<uint32_t>(ns0);
+    cidx = dev.arena.take<uint32_t>(ns0);
+    flags = dev.arena.take<uint32_t>(ns0);
+    pos = dev.arena.take<uint32_t>(ns0);
+    ccount = dev.arena.take<uint32_t>(16);
+    okA = dev.arena.take<uint32_t>(ns1);
+    ovA = dev.arena.take<uint32_t>(ns1 * xw);
+    okB = dev.arena.take<uint32_t>(ns1);
+    ovB = dev.arena.take<uint32_t>(ns1 * xw);
+    buckets = dev.arena.take<uint32_t>(nb * xw);
+    Y = dev.arena.take<uint32_t>((size_t)s.W * s.NY * xw);
+    P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * xw);
+    exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
+    size_t cub2 = 0;
+    if (lds_sort)
+      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, counts, offsets, (int)(nb + 1), st));
+    else
+      ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, dig, skeys, vals, list, (int)maxent, 0,
+                                                  bits_for(nb), st));
+    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
+    if (cub2 > cub) cub = cub2;
+    cubtmp = dev.arena.take<char>(cub);
   }
-  prof.mark("sort");
-  const bool timed = wbase == 0;
-  if (timed) timer_begin(dev);
-  // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
-  hipLaunchKernelGGL(k_accum<C>, dim3(div_up(ns0 / 2, 256)), dim3(256), 0, st, pts_int, list, offsets,
-                     (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0, ivals0, (uint32_t)ns0);
-  ZK_CHECK(hipGetLastError());
-  if (timed) timer_end(dev);
-  prof.mark("accum");
-  // stitch levels: compact the partial items, sum them per bucket (k_stitch_blk), repeat
-  const uint32_t *inK = ikeys0, *inV = ivals0;
-  size_t slots = ns0;
-  uint32_t *outK = okA, *outV = ovA, *altK = okB, *altV = ovB;
-  auto stitch_level = [&]() -> bool {  // true: every item completed at this level
+  void mark(const char *what) {  // the phase profile follows the first group's stream
+    if (prof && wbase == 0) prof->mark(what);
+  }
+
+  void sort() {
+    const int n = s.n, c = s.c;
+    const int kbits = bits_for(nb);  // radix sort: ranks < nb, zero digits nb
+    if (lds_sort) {
+      hipLaunchKernelGGL((k_digits<C, false>), dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff,
+                         sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig, (uint32_t *)nullptr);
+      ZK_CHECK(hipGetLastError());
+      mark("digits");
+      // M entries per workgroup: at least B (so each workgroup's B bucket atomics stay below
+      // its entry count) and enough workgroups to cover the CUs
+      int M = (int)std::max<size_t>((size_t)s.B, ((size_t)n * s.W + 511) / 512);
+      M = (M + 1023) & ~1023;
+      const dim3 grid(div_up(n, M), s.W);
+      const size_t lds = (size_t)s.B * 4;
+      ZK_CHECK(hipFuncSetAttribute((const void *)k_bucket_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+      ZK_CHECK(hipFuncSetAttribute((const void *)k_bucket_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+      ZK_CHECK(hipMemsetAsync(counts, 0, (nb + 1) * 4, st));
+      hipLaunchKernelGGL(k_bucket_lds<false>, grid, dim3(1024), lds, st, dig, n, M, c, counts, (uint32_t *)nullptr);
+      ZK_CHECK(hipGetLastError());
+      size_t cb = cub;
+      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, counts, offsets, (int)(nb + 1), st));
+      ZK_CHECK(hipMemcpyAsync(counts, offsets, nb * 4, hipMemcpyDeviceToDevice, st));  // slot cursors
+      hipLaunchKernelGGL(k_bucket_lds<true>, grid, dim3(1024), lds, st, dig, n, M, c, counts, list);
+      ZK_CHECK(hipGetLastError());
+    } else {
+      hipLaunchKernelGGL((k_digits<C, true>), dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff,
+                         sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig, vals);
+      ZK_CHECK(hipGetLastError());
+      mark("digits");
+      size_t cb = cub;
+      ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cb, dig, skeys, vals, list, (int)maxent, 0, kbits, st));
+      hipLaunchKernelGGL(k_offsets_scan, dim3(div_up(maxent, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
+                         (uint32_t)nb, offsets);
+      ZK_CHECK(hipGetLastError());
+    }
+    mark("sort");
+  }
+
+  void accumulate() {
+    timer_begin(dev, timer_slot, st);
+    // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
+    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(ns0 / 2, 256)), dim3(256), 0, st, pts_int, list, offsets,
+                       (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0, ivals0, (uint32_t)ns0);
+    ZK_CHECK(hipGetLastError());
+    timer_end(dev, timer_slot, st);
+    mark("accum");
+    inK = ikeys0;
+    inV = ivals0;
+    slots = ns0;
+    outK = okA; outV = ovA; altK = okB; altV = ovB;
+  }
+
+  // stitch level: compact the partial items, sum them per bucket (k_stitch_blk); true when
+  // every item completed at this level
+  bool stitch_level() {
     hipLaunchKernelGGL(k_item_flags, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, (const uint32_t *)nullptr,
                        (uint32_t)slots, (uint32_t)nb, flags);
     ZK_CHECK(hipGetLastError());
@@ -1006,11 +1046,11 @@ static void msm_group(Device &dev, const MsmShape &s, const ScalarSlice &sc, int
     uint32_t *tk = outK, *tv = outV;
     outK = altK; outV = altV; altK = tk; altV = tv;
     return final_level;
-  };
+  }
+
   // Y sums, job sums, export and the copy back to the host
-  const int ngrp = s.W * s.J;
-  const size_t expbytes = (size_t)ngrp * 4 * C::NP64 * 8;
-  auto reduce_tail = [&]() {
+  void reduce_tail() {
+    const int c = s.c;
     const int n0 = s.r0.count * s.r0.G, n1 = s.r1.count * s.r1.G;
     if (n0 % 256 == 0 && n1 % 256 == 0) {  // block-level Y sums (every shape from c = 12 up)
       const unsigned nblk = (unsigned)(s.W * (n0 + n1) / 256);
@@ -1022,7 +1062,7 @@ static void msm_group(Device &dev, const MsmShape &s, const ScalarSlice &sc, int
                          s.r1, s.ylanes, Y);
     }
     ZK_CHECK(hipGetLastError());
-    prof.mark("ysum");
+    mark("ysum");
     int jl = 0;  // logical lanes per window, G <= 16
     for (int j = 0; j < c; j++) {
       const int nj = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
@@ -1033,35 +1073,41 @@ static void msm_group(Device &dev, const MsmShape &s, const ScalarSlice &sc, int
     const size_t lanes = (size_t)s.W * wl;
     hipLaunchKernelGGL(k_jobsum_quad<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, wl, P0);
     ZK_CHECK(hipGetLastError());
-    prof.mark("jobsum");
+    mark("jobsum");
+    const int ngrp = s.W * s.J;
     hipLaunchKernelGGL(k_export<C>, dim3(div_up(ngrp, 64)), dim3(64), 0, st, P0, ngrp, exp);
     ZK_CHECK(hipGetLastError());
-    ZK_CHECK(hipMemcpyAsync(h, exp, expbytes, hipMemcpyDeviceToHost, st));
-  };
-  // Levels 0..2 and the whole tail are enqueued without a host round trip: for
-  // well-spread scalars they complete every bucket.  Only when level 2 still leaves more
-  // than one chunk of items (skewed scalars) does the host run further levels and redo the
-  // tail.
-  constexpr int SPECULATIVE_LEVELS = 3;
-  bool done = false;
-  for (int lv = 0; lv < SPECULATIVE_LEVELS && !done; lv++) done = stitch_level();
-  prof.mark("stitch");
-  if (!done) ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
-  reduce_tail();
-  ZK_CHECK(hipStreamSynchronize(st));
-  if (!done && *hc > (uint32_t)STITCH_BS) {
-    for (;;) {
-      if (stitch_level()) break;
-      ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
-      ZK_CHECK(hipStreamSynchronize(st));
-      if (*hc <= (uint32_t)STITCH_BS) break;  // this level's stitch had one chunk: all complete
-    }
-    reduce_tail();
-    ZK_CHECK(hipStreamSynchronize(st));
+    ZK_CHECK(hipMemcpyAsync(h, exp, (size_t)ngrp * 4 * C::NP64 * 8, hipMemcpyDeviceToHost, st));
   }
-  if (timed) timer_collect(dev);
-  prof.mark("export");
-}
+
+  // Levels 0..2 and the whole tail are enqueued without a host round trip: for
+  // well-spread scalars they complete every bucket.
+  static constexpr int SPECULATIVE_LEVELS = 3;
+  void launch() {
+    sort();
+    accumulate();
+    for (int lv = 0; lv < SPECULATIVE_LEVELS && !done; lv++) done = stitch_level();
+    mark("stitch");
+    if (!done) ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
+    reduce_tail();
+  }
+  // Only when level 2 still left more than one chunk of items (skewed scalars) does the
+  // host run further levels and redo the tail.
+  void finish() {
+    ZK_CHECK(hipStreamSynchronize(st));
+    if (!done && *hc > (uint32_t)STITCH_BS) {
+      for (;;) {
+        if (stitch_level()) break;
+        ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
+        ZK_CHECK(hipStreamSynchronize(st));
+        if (*hc <= (uint32_t)STITCH_BS) break;  // this level's stitch had one chunk: all complete
+      }
+      reduce_tail();
+      ZK_CHECK(hipStreamSynchronize(st));
+    }
+    mark("export");
+  }
+};
 
 // host: combine the per-(window, job) sums (XYZZ, canonical reference form; job order
 // of k_jobsum: total, U_{0,0..l0-1}, U_{1,0..l1-1}):
@@ -1154,11 +1200,18 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   const size_t per_w = (size_t)c * 4 * C::NP64;  // exported u64 per window
   uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging((size_t)W * per_w * 8 + 64));
   uint32_t *hc = reinterpret_cast<uint32_t *>(h + (size_t)W * per_w);  // stitch item count
+  // Window groups run one after the other on the device's stream.  (Running two groups
+  // concurrently on two streams -- one's sort and latency-bound tail beside the other's
+  // accumulation -- was measured and does not pay: the two accumulations overlap each
+  // other instead, profiles/r02t_pipelined_groups_ab.txt.)
   for (int wbase = 0; wbase < W; wbase += Wg) {
     dev.arena.rewind(mark);
     const MsmShape sg = (wbase + Wg <= W) ? s : make_shape(n, c, W - wbase);
-    msm_group<C>(dev, sg, sc, wbase, pts_int, h + (size_t)wbase * per_w, hc, prof);
+    GroupPass<C> pass(dev, sg, sc, wbase, pts_int, h + (size_t)wbase * per_w, hc, &prof, st, wbase == 0 ? 0 : -1);
+    pass.launch();
+    pass.finish();
   }
+  timer_collect(dev);
   const auto t0 = std::chrono::steady_clock::now();
   finish_host<C>(c, W, h, out);
   prof.report(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());

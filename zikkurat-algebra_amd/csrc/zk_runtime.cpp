@@ -56,31 +56,37 @@ static std::atomic<bool> g_timer_on{false};
 
 void timer_set_enabled(bool on) { g_timer_on.store(on); }
 
-void timer_begin(Device &dev) {
+void timer_begin(Device &dev, int slot, hipStream_t st) {
+  if (slot < 0 || slot > 1) return;
   if (!g_timer_on.load()) {
-    dev.timer.armed = false;
+    dev.timer.armed[slot] = false;
     return;
   }
-  if (!dev.timer.ev0) {  // created on the device whose stream records them (the caller's)
-    ZK_CHECK(hipEventCreate(&dev.timer.ev0));
-    ZK_CHECK(hipEventCreate(&dev.timer.ev1));
+  if (!dev.timer.ev0[slot]) {  // created on the device whose streams record them (the caller's)
+    ZK_CHECK(hipEventCreate(&dev.timer.ev0[slot]));
+    ZK_CHECK(hipEventCreate(&dev.timer.ev1[slot]));
   }
-  dev.timer.armed = true;
-  ZK_CHECK(hipEventRecord(dev.timer.ev0, dev.stream));
+  dev.timer.armed[slot] = true;
+  dev.timer.counted = true;
+  ZK_CHECK(hipEventRecord(dev.timer.ev0[slot], st ? st : dev.stream));
 }
 
-void timer_end(Device &dev) {
-  if (dev.timer.armed) ZK_CHECK(hipEventRecord(dev.timer.ev1, dev.stream));
+void timer_end(Device &dev, int slot, hipStream_t st) {
+  if (slot < 0 || slot > 1) return;
+  if (dev.timer.armed[slot]) ZK_CHECK(hipEventRecord(dev.timer.ev1[slot], st ? st : dev.stream));
 }
 
 void timer_collect(Device &dev) {
-  if (!dev.timer.armed) return;
-  float ms = 0;
-  ZK_CHECK(hipEventSynchronize(dev.timer.ev1));
-  ZK_CHECK(hipEventElapsedTime(&ms, dev.timer.ev0, dev.timer.ev1));
-  dev.timer.total_ms += ms;
-  dev.timer.launches++;
-  dev.timer.armed = false;
+  for (int k = 0; k < 2; k++) {
+    if (!dev.timer.armed[k]) continue;
+    float ms = 0;
+    ZK_CHECK(hipEventSynchronize(dev.timer.ev1[k]));
+    ZK_CHECK(hipEventElapsedTime(&ms, dev.timer.ev0[k], dev.timer.ev1[k]));
+    dev.timer.total_ms += ms;
+    dev.timer.armed[k] = false;
+  }
+  if (dev.timer.counted) dev.timer.launches++;
+  dev.timer.counted = false;
 }
 
 void timer_reset_all() {

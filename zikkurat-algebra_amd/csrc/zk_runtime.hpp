@@ -57,9 +57,11 @@ class Arena {
 // Timing probe of the dominant kernel (MSM bucket accumulation / NTT pass chain), used by
 // bench.py.  Per device: its events belong to that device and are only touched while the
 // device's mutex is held (every MSM / NTT call holds it).
+// Two slots (durations added), so a call may time two kernels on different streams.
 struct KernelTimer {
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool armed = false;  // this call recorded ev0
+  hipEvent_t ev0[2] = {nullptr, nullptr}, ev1[2] = {nullptr, nullptr};
+  bool armed[2] = {false, false};  // this call recorded ev0[slot]
+  bool counted = false;            // this call contributes one launch
   double total_ms = 0;
   long launches = 0;
 };
@@ -81,9 +83,9 @@ Device &current_device();
 
 // kernel timer (caller holds dev.mu for begin/end/collect)
 void timer_set_enabled(bool on);
-void timer_begin(Device &dev);    // records ev0 on dev.stream when the timer is enabled
-void timer_end(Device &dev);      // records ev1
-void timer_collect(Device &dev);  // after the stream is synchronised: accumulate ev1 - ev0
+void timer_begin(Device &dev, int slot = 0, hipStream_t st = nullptr);  // records ev0 (slot < 0: no-op)
+void timer_end(Device &dev, int slot = 0, hipStream_t st = nullptr);    // records ev1
+void timer_collect(Device &dev);  // after the streams are synchronised: accumulate the armed slots
 void timer_reset_all();
 void timer_read_all(double *total_ms, long *launches);
 

@@ -2,7 +2,7 @@
 // with -fsanitize=thread by tests/test_native.py: several caller threads (as several
 // devices / Haskell capabilities would) run jobs of different sizes concurrently and
 // back to back; every index must run exactly once per job and every job must see its
-// own function.
+// own function; host_parallel_for_main's caller-side consumer must see every result.
 #include <atomic>
 #include <cstdio>
 #include <thread>
@@ -28,6 +28,25 @@ int main() {
         for (int i = 0; i < n; i++)
           if (hit[i].load() != 1) failures++;
         if (wrong.load()) failures++;
+        // the pipelined form: the caller's main function consumes results while the workers
+        // produce them (the MSM's host Horner chain)
+        std::vector<std::atomic<int>> ready(n);
+        std::vector<int> val(n, 0);
+        for (auto &x : ready) x.store(0);
+        long sum = 0;
+        zk::host_parallel_for_main(
+            n,
+            [&](int i) {
+              val[i] = i + tag;
+              ready[i].store(1, std::memory_order_release);
+            },
+            [&] {
+              for (int i = n - 1; i >= 0; i--) {
+                while (!ready[i].load(std::memory_order_acquire)) std::this_thread::yield();
+                sum += val[i];
+              }
+            });
+        if (sum != (long)n * tag + (long)n * (n - 1) / 2) failures++;
       }
     });
   }

@@ -122,7 +122,53 @@ template <class F> inline void mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
   memcpy(r.v, t, sizeof r.v);
   if (t[N] || geq_p<F>(r.v)) sub_p<F>(r.v);
 }
-template <class F> inline void sqr(Fe<F> &r, const Fe<F> &a) { mul(r, a, a); }
+// Montgomery square (SOS): the 2N-word square with every cross product once, doubled,
+// then N reduction rows -- N(N+1)/2 + N^2 word products instead of 2N^2
+template <class F> inline void sqr(Fe<F> &r, const Fe<F> &a) {
+  constexpr int N = F::N;
+  uint64_t t[2 * N + 1];
+  memset(t, 0, sizeof t);
+  for (int i = 0; i < N; i++) {
+    uint64_t c = 0;
+    for (int j = i + 1; j < N; j++) {
+      const u128 x = (u128)a.v[i] * a.v[j] + t[i + j] + c;
+      t[i + j] = (uint64_t)x;
+      c = (uint64_t)(x >> 64);
+    }
+    t[i + N] = c;
+  }
+  uint64_t top = 0;
+  for (int k = 0; k < 2 * N; k++) {  // double the cross products
+    const uint64_t nt = t[k] >> 63;
+    t[k] = (t[k] << 1) | top;
+    top = nt;
+  }
+  uint64_t c = 0;
+  for (int i = 0; i < N; i++) {  // diagonal
+    const u128 x = (u128)a.v[i] * a.v[i] + t[2 * i] + c;
+    t[2 * i] = (uint64_t)x;
+    const u128 y = (u128)t[2 * i + 1] + (uint64_t)(x >> 64);
+    t[2 * i + 1] = (uint64_t)y;
+    c = (uint64_t)(y >> 64);
+  }
+  t[2 * N] = c;
+  for (int i = 0; i < N; i++) {  // Montgomery reduction rows
+    const uint64_t m = t[i] * F::MINV;
+    uint64_t cc = 0;
+    for (int j = 0; j < N; j++) {
+      const u128 x = (u128)m * F::P[j] + t[i + j] + cc;
+      t[i + j] = (uint64_t)x;
+      cc = (uint64_t)(x >> 64);
+    }
+    for (int k = i + N; cc && k <= 2 * N; k++) {
+      const u128 y = (u128)t[k] + cc;
+      t[k] = (uint64_t)y;
+      cc = (uint64_t)(y >> 64);
+    }
+  }
+  memcpy(r.v, t + N, sizeof r.v);
+  if (t[2 * N] || geq_p<F>(r.v)) sub_p<F>(r.v);
+}
 
 // standard <-> Montgomery
 template <class F> inline void to_mont(Fe<F> &r, const Fe<F> &a) {
@@ -427,6 +473,110 @@ template <class F> inline void xyzz_add(Xyzz<F> &r, const Xyzz<F> &a, const Xyzz
   mul(t, a.ZZZ, b.ZZZ);
   mul(r.ZZZ, t, PPP);
 }
+// Jacobian (x = X/Z^2, y = Y/Z^3; infinity Z == 0), a = 0: the host Horner chain's
+// doublings cost 2M + 5S here against 6M + 3S in XYZZ
+template <class F>
+struct Jac {
+  Fe<F> X, Y, Z;
+};
+template <class F> inline bool jac_is_inf(const Jac<F> &a) { return is_zero(a.Z); }
+template <class F> inline void jac_set_inf(Jac<F> &r) {
+  set_one(r.X);
+  set_one(r.Y);
+  set_zero(r.Z);
+}
+// dbl-2009-l
+template <class F> inline void jac_dbl(Jac<F> &r, const Jac<F> &p) {
+  if (jac_is_inf(p)) { r = p; return; }
+  Fe<F> A, B, C, D, E, Fv, t;
+  sqr(A, p.X);
+  sqr(B, p.Y);
+  sqr(C, B);
+  add(t, p.X, B);
+  sqr(t, t);
+  sub(t, t, A);
+  sub(t, t, C);
+  add(D, t, t);
+  add(E, A, A);
+  add(E, E, A);
+  sqr(Fv, E);
+  Fe<F> X3, Z3;
+  sub(X3, Fv, D);
+  sub(X3, X3, D);
+  mul(Z3, p.Y, p.Z);
+  add(r.Z, Z3, Z3);
+  sub(t, D, X3);
+  mul(t, E, t);
+  add(C, C, C);
+  add(C, C, C);
+  add(C, C, C);
+  sub(r.Y, t, C);
+  r.X = X3;
+}
+// add-2007-bl, all special cases
+template <class F> inline void jac_add(Jac<F> &r, const Jac<F> &a, const Jac<F> &b) {
+  if (jac_is_inf(b)) { r = a; return; }
+  if (jac_is_inf(a)) { r = b; return; }
+  Fe<F> Z1Z1, Z2Z2, U1, U2, S1, S2, t;
+  sqr(Z1Z1, a.Z);
+  sqr(Z2Z2, b.Z);
+  mul(U1, a.X, Z2Z2);
+  mul(U2, b.X, Z1Z1);
+  mul(t, b.Z, Z2Z2);
+  mul(S1, a.Y, t);
+  mul(t, a.Z, Z1Z1);
+  mul(S2, b.Y, t);
+  Fe<F> H, R;
+  sub(H, U2, U1);
+  sub(R, S2, S1);
+  if (is_zero(H)) {
+    if (is_zero(R)) jac_dbl(r, a);
+    else jac_set_inf(r);
+    return;
+  }
+  add(R, R, R);
+  Fe<F> I, J, V, X3;
+  add(I, H, H);
+  sqr(I, I);
+  mul(J, H, I);
+  mul(V, U1, I);
+  sqr(X3, R);
+  sub(X3, X3, J);
+  sub(X3, X3, V);
+  sub(X3, X3, V);
+  sub(t, V, X3);
+  mul(t, R, t);
+  mul(S1, S1, J);
+  add(S1, S1, S1);
+  Fe<F> Z3;
+  add(Z3, a.Z, b.Z);
+  sqr(Z3, Z3);
+  sub(Z3, Z3, Z1Z1);
+  sub(Z3, Z3, Z2Z2);
+  mul(r.Z, Z3, H);
+  sub(r.Y, t, S1);
+  r.X = X3;
+}
+// XYZZ -> Jacobian with Z = ZZ ZZZ: X ZZ ZZZ^2, Y ZZ^3 ZZZ^2
+template <class F> inline void xyzz_to_jac(Jac<F> &r, const Xyzz<F> &a) {
+  if (xyzz_is_inf(a)) { jac_set_inf(r); return; }
+  Fe<F> z3s, t, u;
+  sqr(z3s, a.ZZZ);
+  mul(t, a.ZZ, z3s);   // ZZ ZZZ^2
+  mul(r.X, a.X, t);
+  sqr(u, a.ZZ);
+  mul(u, u, t);        // ZZ^3 ZZZ^2
+  mul(r.Y, a.Y, u);
+  mul(r.Z, a.ZZ, a.ZZZ);
+}
+template <class F> inline void jac_to_xyzz(Xyzz<F> &r, const Jac<F> &a) {
+  if (jac_is_inf(a)) { xyzz_set_inf(r); return; }
+  r.X = a.X;
+  r.Y = a.Y;
+  sqr(r.ZZ, a.Z);
+  mul(r.ZZZ, r.ZZ, a.Z);
+}
+
 // -> homogeneous projective (X ZZZ : Y ZZ : ZZ ZZZ)
 template <class F> inline void xyzz_to_proj(Proj<F> &r, const Xyzz<F> &a) {
   if (xyzz_is_inf(a)) { proj_set_inf(r); return; }

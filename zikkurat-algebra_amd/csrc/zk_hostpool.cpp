@@ -60,13 +60,14 @@ struct HostPool {
       job->drain();
     }
   }
-  void run(int count, const std::function<void(int)> &f) {
+  void run(int count, const std::function<void(int)> &f, const std::function<void()> *main_fn = nullptr) {
     auto job = std::make_shared<Job>(&f, count);
     {
       std::lock_guard<std::mutex> lk(mu);
       active.push_back(job);
     }
     cv.notify_all();
+    if (main_fn) (*main_fn)();
     job->drain();
     while (job->done.load(std::memory_order_acquire) < count) std::this_thread::yield();
     std::lock_guard<std::mutex> lk(mu);
@@ -79,14 +80,29 @@ struct HostPool {
 };
 }  // namespace
 
+static HostPool *shared_pool() {
+  static HostPool *pool = new HostPool();  // leaked on purpose: detached workers outlive static teardown
+  return pool;
+}
+
 void host_parallel_for(int n, const std::function<void(int)> &fn) {
   if (n <= 0) return;
-  static HostPool *pool = new HostPool();  // leaked on purpose: detached workers outlive static teardown
+  HostPool *pool = shared_pool();
   if (n == 1 || pool->workers == 0) {
     for (int i = 0; i < n; i++) fn(i);
     return;
   }
   pool->run(n, fn);
+}
+
+void host_parallel_for_main(int n, const std::function<void(int)> &fn, const std::function<void()> &main_fn) {
+  HostPool *pool = shared_pool();
+  if (n <= 0 || pool->workers == 0) {
+    for (int i = 0; i < n; i++) fn(i);
+    main_fn();
+    return;
+  }
+  pool->run(n, fn, &main_fn);
 }
 
 }  // namespace zk

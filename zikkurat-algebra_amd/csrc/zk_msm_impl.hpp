@@ -21,7 +21,7 @@
 //                     segmented scans, level after level: no serial loop anywhere, so
 //                     skewed scalars (all equal, carry windows) stay fast
 //   4. k_ysum(2)      digit split of the bucket weights into plain sums Y0, Y1
-//   5. k_jobsum_quad  the weighted Y sums by bit jobs (quad-cooperative additions)
+//   5. k_jobsum_blk   the weighted Y sums by bit jobs (a block of quad-cooperative additions per job)
 //   6. host           Horner over the power-of-two exponents and the windows
 // Windows are processed in groups when W n exceeds one pass's sort capacity.
 //
@@ -32,6 +32,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <memory>
+#include <thread>
 #include <vector>
 #include "zk_curve.hpp"
 #include "zk_host.hpp"
@@ -679,54 +681,53 @@ __device__ __forceinline__ void xyzz_add_quad(Xyzz<F> &acc, const Xyzz<F> &b, ui
   acc.ZZ = ZZ3;
 }
 
-// 7'. k_jobsum on quads: one logical lane = 4 physical lanes (xyzz_add_quad), segment folds
-//     across quads; jlanes counts PHYSICAL lanes (4 x logical, multiple of 64), G <= 16.
+// 7. weighted Y sums by bit jobs: one 256-thread block per (window, job) = 64 quad lanes
+//    (xyzz_add_quad: 4 physical lanes per addition).  Job 0 is the total sum_m B_m, taken
+//    over the 2^l1 sums Y1 (the smaller set); job j in 1..l0 sums the Y0_v with bit j-1 of v
+//    set, job j > l0 the Y1_v with bit j-1-l0 set (exponent j-1 either way).  Each quad adds
+//    n/64 <= 2 items, then a block fold through LDS: depth log2(n) quad additions, where a
+//    fold inside one wavefront (16 quads) would leave 8-16 items serial per quad.
 template <class C>
-__global__ void __launch_bounds__(256) k_jobsum_quad(const uint32_t *__restrict__ Y, int W, int c, int l0, int QA,
-                                                     int wlanes, uint32_t *__restrict__ out) {
+__global__ void __launch_bounds__(256) k_jobsum_blk(const uint32_t *__restrict__ Y, int c, int l0,
+                                                    uint32_t *__restrict__ out) {
   using F = typename C::Fp;
-  __shared__ uint32_t park_lds[256 * xyzz_words<F>()];
-  uint32_t *park = park_lds + threadIdx.x * xyzz_words<F>();
+  constexpr int XW = xyzz_words<F>();
+  __shared__ uint32_t park_lds[256 * XW];  // xyzz_add_quad's doubling fallback, per lane
+  __shared__ uint4 fold4[32 * XW / 4];     // fold exchange, one slot per upper-half quad
+  uint32_t *fold = reinterpret_cast<uint32_t *>(fold4);
+  uint32_t *park = park_lds + threadIdx.x * XW;
   const int l1 = c - 1 - l0;
   const int NY = (1 << l0) + (1 << l1);
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  const int w = g / wlanes, t = (g % wlanes) >> 2;  // logical lane within the window
-  const bool active = w < W;
-  int j = -1, G = 1, lane = 0, off = 0;
-  for (int jj = 0; jj < c; jj++) {
-    const int n = jj == 0 ? (1 << l0) : (jj <= l0 ? (1 << (l0 - 1)) : (1 << (l1 - 1)));
-    int Gj = n / QA;
-    Gj = Gj < 1 ? 1 : (Gj > 16 ? 16 : Gj);
-    if (t >= off && t < off + Gj) { j = jj; G = Gj; lane = t - off; }
-    off += Gj;
-  }
+  const int w = blockIdx.x / c, j = blockIdx.x % c;
+  const int t = threadIdx.x >> 2;  // quad (logical lane) 0..63
+  const int d = (j == 0 || j > l0) ? 1 : 0;  // Y1 or Y0
+  const int b = j == 0 ? -1 : (d ? j - 1 - l0 : j - 1);
+  const int ld = d ? l1 : l0;
+  const int n = b < 0 ? (1 << ld) : (1 << (ld - 1));
+  const uint32_t *Yd = Y + ((size_t)w * NY + (d ? (1 << l0) : 0)) * XW;
   Xyzz<F> acc;
   xyzz_set_inf(acc);
-  if (active && j >= 0) {
-    const int d = (j == 0 || j <= l0) ? 0 : 1;
-    const int b = j == 0 ? -1 : (d == 0 ? j - 1 : j - 1 - l0);
-    const int ld = d ? l1 : l0;
-    const int n = (b < 0) ? (1 << ld) : (1 << (ld - 1));
-    const int per = n / G;
-    const uint32_t *Yd = Y + ((size_t)w * NY + (d ? (1 << l0) : 0)) * xyzz_words<F>();
-    for (int k = 0; k < per; k++) {
-      const int e = lane * per + k;
-      int v = e;
-      if (b >= 0) {
-        const int lowmask = (1 << b) - 1;
-        v = ((e & ~lowmask) << 1) | (1 << b) | (e & lowmask);
-      }
-      Xyzz<F> p;
-      xyzz_load(p, Yd + (size_t)v * xyzz_words<F>());
-      xyzz_add_quad(acc, p, park);
+  for (int e = t; e < n; e += 64) {
+    int v = e;
+    if (b >= 0) {  // e-th index with bit b set
+      const int lowmask = (1 << b) - 1;
+      v = ((e & ~lowmask) << 1) | (1 << b) | (e & lowmask);
     }
+    Xyzz<F> p;
+    xyzz_load(p, Yd + (size_t)v * XW);
+    xyzz_add_quad(acc, p, park);
   }
-  for (int o = G >> 1; o >= 1; o >>= 1) {
-    Xyzz<F> other = xyzz_shfl_down(acc, 4 * o, 4 * G);
-    xyzz_add_quad(acc, other, park);
+  for (int h = 32; h >= 1; h >>= 1) {
+    if (t >= h && t < 2 * h && (threadIdx.x & 3) == 0) xyzz_store(fold + (size_t)(t - h) * XW, acc);
+    __syncthreads();
+    if (t < h) {
+      Xyzz<F> o;
+      xyzz_load(o, fold + (size_t)t * XW);
+      xyzz_add_quad(acc, o, park);
+    }
+    __syncthreads();
   }
-  if (active && j >= 0 && lane == 0 && (threadIdx.x & 3) == 0)
-    xyzz_store(out + ((size_t)w * c + j) * xyzz_words<F>(), acc);
+  if (threadIdx.x == 0) xyzz_store(out + ((size_t)w * c + j) * XW, acc);
 }
 
 // export: XYZZ (device form) -> canonical reference-form coordinates, 4 x NP64 u64
@@ -753,7 +754,7 @@ __global__ void k_export(const uint32_t *__restrict__ in, int n, uint64_t *__res
 // host orchestration
 
 struct MsmShape {
-  int n, c, W, B, l0, l1, NY, QY, J, CH, QA;  // W: windows handled by one pass of the pipeline
+  int n, c, W, B, l0, l1, NY, QY, J, CH;  // W: windows handled by one pass of the pipeline
   SegRegion r0, r1;
   int ylanes;  // lanes per window of k_ysum (multiple of 64)
 };
@@ -762,8 +763,7 @@ static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; retu
 
 // Shape of one pipeline pass over W windows of n scalars.  The constants were swept on
 // MI355X (profiles/r01_*, profiles/r02h_qy_qa_sweep.txt): Y sums take 16 buckets per lane at
-// scale (8: ysum 0.37 -> 0.48 ms, 4: 0.66 ms at BLS12-381 2^20), the weighted job sums 8
-// items per lane (4: no change), the accumulation 64 sorted entries per lane (128 from 2^25
+// scale (8: ysum 0.37 -> 0.48 ms, 4: 0.66 ms at BLS12-381 2^20), the accumulation 64 sorted entries per lane (128 from 2^25
 // entries on, profiles/r01_v7_ch_sweep.txt).
 static MsmShape make_shape(int n, int c, int W) {
   MsmShape s;
@@ -776,13 +776,14 @@ static MsmShape make_shape(int n, int c, int W) {
   s.NY = (1 << s.l0) + (1 << s.l1);
   auto pow2 = [](int v) { int r = 1; while (2 * r <= v) r *= 2; return r; };  // segments need powers of 2
   // buckets per lane in the Y sums: 16 at scale, fewer when there are few buckets, so the
-  // sums keep ~64K lanes (2 W B bucket adds) instead of a long serial chain
+  // sums keep at most ~64K lanes (2 W B bucket adds): one wave per SIMD, each issuing its
+  // own chain (more lanes share the SIMDs and only lengthen every fold step; BLS12-381
+  // 2^16: ysum 0.21 -> ~0.15 ms with QY 2 -> 4, profiles/r02y_msm_small_ab.txt)
   {
     const size_t adds = 2 * (size_t)s.W * (size_t)s.B;
-    int q = (int)(adds >> 16);
+    int q = (int)((adds + 65535) >> 16);  // rounded up: at most ~64K lanes, one wave per SIMD
     q = q < 1 ? 1 : (q > 16 ? 16 : q);
-    s.QY = pow2(q);
-  }
+    s.QY = pow2(q) < q ? 2 * pow2(q) : pow2(q);  }
   auto clampG = [](int g) { return g < 1 ? 1 : (g > 64 ? 64 : g); };
   s.r0 = SegRegion{1 << s.l1, clampG((1 << s.l0) / s.QY), 1 << s.l0};  // Y1 sums
   s.r1 = SegRegion{1 << s.l0, clampG((1 << s.l1) / s.QY), 1 << s.l1};  // Y0 sums
@@ -796,7 +797,6 @@ static MsmShape make_shape(int n, int c, int W) {
     s.CH = ch >= 64 ? 64 : (ch <= 4 ? 4 : (int)ch);
     if (ent >= ((size_t)1 << 25)) s.CH = 128;
   }
-  s.QA = 8;  // items per lane in the weighted job sums
   return s;
 }
 
@@ -1063,15 +1063,7 @@ struct GroupPass {
     }
     ZK_CHECK(hipGetLastError());
     mark("ysum");
-    int jl = 0;  // logical lanes per window, G <= 16
-    for (int j = 0; j < c; j++) {
-      const int nj = j == 0 ? (1 << s.l0) : (j <= s.l0 ? (1 << (s.l0 - 1)) : (1 << (s.l1 - 1)));
-      int g = nj / s.QA;
-      jl += g < 1 ? 1 : (g > 16 ? 16 : g);
-    }
-    const int wl = ((jl + 15) & ~15) * 4;
-    const size_t lanes = (size_t)s.W * wl;
-    hipLaunchKernelGGL(k_jobsum_quad<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, Y, s.W, c, s.l0, s.QA, wl, P0);
+    hipLaunchKernelGGL(k_jobsum_blk<C>, dim3((unsigned)(s.W * c)), dim3(256), 0, st, Y, c, s.l0, P0);
     ZK_CHECK(hipGetLastError());
     mark("jobsum");
     const int ngrp = s.W * s.J;
@@ -1113,16 +1105,20 @@ struct GroupPass {
 // of k_jobsum: total, U_{0,0..l0-1}, U_{1,0..l1-1}):
 //   V_w = sum_j 2^(e_j) P_{w,j}, e_j = 0 (total), j - 1 (bit jobs)   [Horner over c - 1 exponents]
 //   result = sum_w 2^(c w) V_w                                        [Horner over the windows]
-// The V_w are independent: they run on the host thread pool; the cross-window chain of
-// c (W - 1) doublings is the only serial part.  On one host core a point op costs ~0.4 us
-// against ~20 us for a lone GPU lane, which is why this tail stays on the host.
+// The V_w are independent: the host pool computes them, top window first, WHILE the calling
+// thread runs the cross-window chain of c (W - 1) doublings (Jacobian, 2M + 5S each),
+// waiting for each V_w only when the chain reaches it.  On one host core a point op costs
+// ~0.4 us against ~20 us for a lone GPU lane, which is why this tail stays on the host.
 template <class C>
 static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typename HostOf<C>::Fp> &out) {
   using HF = typename HostOf<C>::Fp;
   const int NP = C::NP64;
   const int J = c, E = c - 1;  // local exponents 0 .. c-2
-  std::vector<zkh::Xyzz<HF>> V(W);
-  host_parallel_for(W, [&](int w) {
+  std::vector<zkh::Jac<HF>> V(W);
+  std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[W]);
+  for (int w = 0; w < W; w++) ready[w].store(0, std::memory_order_relaxed);
+  auto window = [&](int i) {
+    const int w = W - 1 - i;
     std::vector<zkh::Xyzz<HF>> Z(E);
     for (auto &z : Z) zkh::xyzz_set_inf(z);
     for (int j = 0; j < J; j++) {
@@ -1142,13 +1138,20 @@ static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typena
       zkh::xyzz_dbl(acc, acc);
       zkh::xyzz_add(acc, acc, Z[e]);
     }
-    V[w] = acc;
-  });
-  zkh::xyzz_set_inf(out);
-  for (int w = W - 1; w >= 0; w--) {
-    for (int k = 0; k < c; k++) zkh::xyzz_dbl(out, out);
-    zkh::xyzz_add(out, out, V[w]);
-  }
+    zkh::xyzz_to_jac(V[w], acc);
+    ready[w].store(1, std::memory_order_release);
+  };
+  zkh::Jac<HF> acc;
+  zkh::jac_set_inf(acc);
+  auto chain = [&] {
+    for (int w = W - 1; w >= 0; w--) {
+      for (int k = 0; k < c; k++) zkh::jac_dbl(acc, acc);
+      while (!ready[w].load(std::memory_order_acquire)) std::this_thread::yield();
+      zkh::jac_add(acc, acc, V[w]);
+    }
+  };
+  host_parallel_for_main(W, window, chain);
+  zkh::jac_to_xyzz(out, acc);
 }
 
 // Run the device pipeline for one scalar slice.  points are DEVICE pointers (or host

@@ -20,7 +20,7 @@ import glob
 import json
 from collections import defaultdict
 
-STREAMING_X2 = ("k_ntt_pass", "k_points_int", "k_digits", "k_bucket_lds", "k_export", "k_arr", "k_ysum")
+STREAMING_X2 = ("k_ntt_pass", "k_points_int", "k_digits", "k_coarse", "k_fine", "k_export", "k_arr", "k_ysum")
 GATHER_GLDS = ("k_accum",)
 READS = 1 << 24
 

@@ -10,9 +10,9 @@
 //   0. k_points_int   affine points -> internal radix (one product per coordinate)
 //   1. k_digits       scalar (Montgomery -> standard by REDC, Fr_mont.c:330-335) ->
 //                     signed c-bit digits of every window
-//      k_bucket_lds   bucket sort of the (window, point) entries: LDS counting sort per
-//                     (window, chunk) workgroup -> bucket offsets + bucket-ordered list
-//                     of point index | sign (hipCUB radix sort when c > 16);
+//      k_coarse/k_fine  bucket sort of the (window, point) entries: two-level LDS counting
+//                     sort (coarse bins, then the fine buckets of each bin) -> bucket
+//                     offsets + bucket-ordered list of point index | sign;
 //                     bucket rank = window * B + |digit| - 1
 //   2. k_accum        balanced bucket accumulation: every thread adds exactly CH
 //                     consecutive list entries (mixed XYZZ += affine adds), flushing
@@ -124,85 +124,181 @@ struct DigitStream {
 //    result is the bucket offsets (nb + 1 entries, offsets[nb] = total) and the
 //    bucket-ordered list of point index | sign << 31 (n < 2^31 by the C ABI's int).
 //
-//    c <= 16 (B <= 32768, the 2^10..2^24 shapes): LDS counting sort.  k_digits writes one
-//    u32 per entry (|digit| | sign, window-major); a workgroup owns M entries of ONE window,
-//    counts them in an LDS histogram of its window's B buckets (LDS atomics), and adds the
-//    histogram to the global counts with one coalesced atomic per nonzero bucket; an
-//    exclusive scan gives the offsets; the scatter pass recounts, claims each bucket's slot
-//    range with one atomic per nonzero bucket and hands out slots from LDS.  Global traffic
-//    is ~4 passes of 4 B per entry, and only B atomics per workgroup reach L2 (random
-//    per-entry global atomics measured 5-10x slower).  The order inside a bucket depends on
-//    atomic timing; bucket sums are group sums, so the canonical result does not.
-//    c > 16: hipCUB radix sort of (rank, value) pairs on ceil(log2(nb + 1)) bits.
-template <class C, bool KEYS>
+//    Two-level counting sort, every write coalesced: k_digits writes one u32 per entry
+//    (|digit| | sign, window-major).  Level 1 sorts by COARSE bin = (|digit| - 1) >> s
+//    (MSM_COARSE_BINS bins per window): k_coarse<false> counts each workgroup's entries per
+//    coarse bin in LDS into a (window, bin, workgroup) matrix, an exclusive scan of that
+//    matrix is every workgroup's slot range in every bin, k_coarse<true> scatters
+//    (value, fine index) in runs of ~M / 256 entries per bin.  Level 2 (k_fine): one
+//    workgroup per coarse bin counts its 2^s fine buckets in LDS, writes their offsets and
+//    places its entries inside the bin's own small output range (lines merge in L2).
+//    A single-level scatter of 4-B entries to random buckets measured 600 MB of HBM
+//    writes for 67 MB of entries at BLS12-381 2^20 (profiles/r02j_pmc.json).  The order
+//    inside a bucket depends on atomic timing; bucket sums are group sums, so the
+//    canonical result does not.
+template <class C>
 __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int stride, int loff,
                                                 int nread, int mont, int c, int wbase, int Wg,
-                                                uint32_t *__restrict__ out, uint32_t *__restrict__ vals) {
+                                                uint32_t *__restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   DigitStream<C> ds;
   ds.load(scalars, i, stride, loff, nread, mont);
-  const uint32_t B = 1u << (c - 1);
-  const uint32_t nb = (uint32_t)Wg * B;
   for (int w = 0; w < wbase + Wg; w++) {
     uint32_t sign;
     const uint32_t mag = ds.next(c, sign);
     if (w < wbase) continue;
-    const uint32_t lw = (uint32_t)(w - wbase);
-    if (KEYS) {  // (rank | nb for zero digits, value) pairs for the radix sort
-      out[(size_t)lw * n + i] = mag ? lw * B + mag - 1 : nb;
-      vals[(size_t)lw * n + i] = (uint32_t)i | sign;
-    } else {
-      out[(size_t)lw * n + i] = mag | sign;
+    out[(size_t)(w - wbase) * n + i] = mag | sign;
+  }
+}
+
+constexpr int MSM_COARSE_BINS = 256;  // coarse bins per window (fewer when B is smaller)
+constexpr int SORT_CHUNK = 4096;      // level-1 entries staged in LDS at a time (16 per thread)
+constexpr int FINE_LDS_MAX = 8192;    // level-2 bins up to this size are placed in LDS
+constexpr int FINE_LDS_BYTES = 150 * 1024;  // dynamic LDS of k_fine: 2^s counters + staging
+static int fine_stage_cap(int s) {
+  const int cap = (FINE_LDS_BYTES - (4 << s)) / 4;
+  return cap < FINE_LDS_MAX ? cap : FINE_LDS_MAX;
+}
+
+// block-wide exclusive scan of one value per thread (256 threads); returns the thread's
+// exclusive prefix, *total the sum
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *tmp, uint32_t *total) {
+  const int t = threadIdx.x;
+  tmp[t] = v;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {
+    const uint32_t o = t >= d ? tmp[t - d] : 0;
+    __syncthreads();
+    tmp[t] += o;
+    __syncthreads();
+  }
+  const uint32_t incl = tmp[t];
+  *total = tmp[255];
+  __syncthreads();
+  return incl - v;
+}
+
+// Level 1.  Workgroup (window w = blockIdx.y, entries [blockIdx.x * M, +M)).  Counting
+// pass: per-bin counts into cnt[(w * nbins + bin) * nwg + wg].  Scatter pass: the scanned
+// matrix gives this workgroup's first slot in every bin; entries go through LDS in chunks,
+// sorted by bin there, so every bin's run leaves as consecutive lanes' stores.
+template <bool SCATTER>
+__global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig, int n, int M, int s, int nbins,
+                                                uint32_t *__restrict__ cnt, uint32_t *__restrict__ tmpv,
+                                                uint16_t *__restrict__ tmpf) {
+  __shared__ uint32_t hist[MSM_COARSE_BINS], lofs[MSM_COARSE_BINS], gcur[MSM_COARSE_BINS], scan_tmp[256];
+  __shared__ uint32_t sv[SORT_CHUNK], sk[SORT_CHUNK];
+  const uint32_t w = blockIdx.y, g = blockIdx.x, nwg = gridDim.x;
+  const int t = threadIdx.x;
+  const int e0 = (int)g * M, e1 = min(n, e0 + M);
+  const uint32_t *d = dig + (size_t)w * n;
+  uint32_t *cw = cnt + (size_t)w * nbins * nwg + g;
+  if (!SCATTER) {
+    if (w == 0 && g == 0 && t == 0) cnt[(size_t)gridDim.y * nbins * nwg] = 0;  // the scan's total slot
+    for (int b = t; b < nbins; b += 256) hist[b] = 0;
+    __syncthreads();
+    for (int e = e0 + t; e < e1; e += 256) {
+      const uint32_t mag = d[e] & 0x7fffffffu;
+      if (mag) atomicAdd(&hist[(mag - 1) >> s], 1u);
+    }
+    __syncthreads();
+    for (int b = t; b < nbins; b += 256) cw[(size_t)b * nwg] = hist[b];
+    return;
+  }
+  for (int b = t; b < nbins; b += 256) gcur[b] = cw[(size_t)b * nwg];
+  const uint32_t fmask = (1u << s) - 1;
+  constexpr int PER = SORT_CHUNK / 256;
+  for (int c0 = e0; c0 < e1; c0 += SORT_CHUNK) {
+    for (int b = t; b < nbins; b += 256) hist[b] = 0;
+    __syncthreads();
+    uint32_t val[PER], key[PER], rank[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const int e = c0 + k * 256 + t;
+      const uint32_t v = e < e1 ? d[e] : 0u;
+      const uint32_t mag = v & 0x7fffffffu;
+      key[k] = 0xffffffffu;
+      if (mag) {
+        const uint32_t b = (mag - 1) >> s;
+        key[k] = (b << 16) | ((mag - 1) & fmask);
+        val[k] = (uint32_t)e | (v & 0x80000000u);
+        rank[k] = atomicAdd(&hist[b], 1u);
+      }
+    }
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t h = t < nbins ? hist[t] : 0u;
+    const uint32_t ex = block_excl_scan256(h, scan_tmp, &tot);
+    if (t < nbins) lofs[t] = ex;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (key[k] != 0xffffffffu) {
+        const uint32_t p = lofs[key[k] >> 16] + rank[k];
+        sv[p] = val[k];
+        sk[p] = key[k];
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < tot; i += 256) {
+      const uint32_t k = sk[i], b = k >> 16;
+      const uint32_t slot = gcur[b] + (i - lofs[b]);
+      tmpv[slot] = sv[i];
+      tmpf[slot] = (uint16_t)(k & 0xffffu);
+    }
+    __syncthreads();
+    if (t < nbins) gcur[t] += h;
+  }
+}
+
+// Level 2.  Workgroup = coarse bin q = w * nbins + b, entries [coff[q * nwg], next bin's
+// start) of the level-1 order; 2^s fine buckets (dynamic LDS: 4 B counters, then the
+// staging area).  A bin of at most `cap` entries is placed in LDS and leaves as one
+// contiguous run; a larger one (skewed scalars) is scattered directly.
+static __global__ void __launch_bounds__(256) k_fine(const uint32_t *__restrict__ coff, int nwg, uint32_t nq, int s,
+                                                     int cap, const uint32_t *__restrict__ tmpv,
+                                                     const uint16_t *__restrict__ tmpf, uint32_t *__restrict__ list,
+                                                     uint32_t *__restrict__ offsets) {
+  extern __shared__ uint32_t fh[];
+  __shared__ uint32_t part[256];
+  const int F = 1 << s, t = threadIdx.x;
+  uint32_t *sv = fh + F;
+  const uint32_t q = blockIdx.x;
+  const uint32_t start = coff[(size_t)q * nwg];
+  const uint32_t end = coff[(size_t)(q + 1) * nwg];  // the matrix carries one extra entry: the total
+  const bool staged = end - start <= (uint32_t)cap;
+  for (int f = t; f < F; f += 256) fh[f] = 0;
+  __syncthreads();
+  for (uint32_t e = start + t; e < end; e += 256) atomicAdd(&fh[tmpf[e]], 1u);
+  __syncthreads();
+  // exclusive scan of the F counters: thread t owns the contiguous span [t * per, +per)
+  const int per = (F + 255) / 256;
+  uint32_t sum = 0;
+  for (int k = 0; k < per; k++) {
+    const int f = t * per + k;
+    if (f < F) sum += fh[f];
+  }
+  uint32_t tot;
+  uint32_t run = block_excl_scan256(sum, part, &tot);
+  for (int k = 0; k < per; k++) {
+    const int f = t * per + k;
+    if (f < F) {
+      const uint32_t h = fh[f];
+      fh[f] = staged ? run : start + run;
+      offsets[(size_t)q * F + f] = start + run;
+      run += h;
     }
   }
-}
-
-// Workgroup (window w = blockIdx.y, entries [blockIdx.x * M, +M)) LDS histogram; the SCATTER
-// pass writes the list, the counting pass adds into `ctr` (counts).
-template <bool SCATTER>
-__global__ void __launch_bounds__(1024) k_bucket_lds(const uint32_t *__restrict__ dig, int n, int M, int c,
-                                                     uint32_t *__restrict__ ctr, uint32_t *__restrict__ list) {
-  extern __shared__ uint32_t hist[];
-  const uint32_t B = 1u << (c - 1);
-  const uint32_t w = blockIdx.y;
-  const int e0 = blockIdx.x * M, e1 = min(n, e0 + M);
-  const uint32_t *d = dig + (size_t)w * n;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) hist[b] = 0;
+  if (q == nq - 1 && t == 0) offsets[(size_t)nq * F] = end;
   __syncthreads();
-  for (int e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-    const uint32_t mag = d[e] & 0x7fffffffu;
-    if (mag) atomicAdd(&hist[mag - 1], 1u);
+  if (staged) {
+    for (uint32_t e = start + t; e < end; e += 256) sv[atomicAdd(&fh[tmpf[e]], 1u)] = tmpv[e];
+    __syncthreads();
+    for (uint32_t i = t; i < end - start; i += 256) list[start + i] = sv[i];
+  } else {
+    for (uint32_t e = start + t; e < end; e += 256) list[atomicAdd(&fh[tmpf[e]], 1u)] = tmpv[e];
   }
-  __syncthreads();
-  uint32_t *g = ctr + (size_t)w * B;
-  for (uint32_t b = threadIdx.x; b < B; b += blockDim.x) {
-    const uint32_t h = hist[b];
-    if (!h) continue;
-    if (SCATTER) hist[b] = atomicAdd(&g[b], h);  // this workgroup's slot range in bucket b
-    else atomicAdd(&g[b], h);
-  }
-  if (!SCATTER) return;
-  __syncthreads();
-  for (int e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-    const uint32_t v = d[e];
-    const uint32_t mag = v & 0x7fffffffu;
-    if (mag) list[atomicAdd(&hist[mag - 1], 1u)] = (uint32_t)e | (v & 0x80000000u);
-  }
-}
-
-// offsets from the radix-sorted ranks (nondecreasing; zero digits rank nb): entry e writes
-// offsets[r] = e for every rank r in (rank(e-1), rank(e)], the last entry fills the ranks
-// after it with M
-static __global__ void __launch_bounds__(256) k_offsets_scan(const uint32_t *__restrict__ skeys, uint32_t M,
-                                                             uint32_t nb, uint32_t *__restrict__ offsets) {
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= M) return;
-  const uint32_t r = min(skeys[e], nb);
-  const uint32_t lo = e ? min(skeys[e - 1], nb) + 1 : 0;
-  for (uint32_t q = lo; q <= r; q++) offsets[q] = e;
-  if (e == M - 1)
-    for (uint32_t q = r + 1; q <= nb; q++) offsets[q] = M;
 }
 
 // first bucket index b with offsets[b+1] > e  (offsets has nb+1 entries)
@@ -757,6 +853,10 @@ struct MsmShape {
   int n, c, W, B, l0, l1, NY, QY, J, CH;  // W: windows handled by one pass of the pipeline
   SegRegion r0, r1;
   int ylanes;  // lanes per window of k_ysum (multiple of 64)
+  // two-level bucket sort: 2^fs fine buckets per coarse bin, nbins coarse bins per window,
+  // level-1 workgroups of M entries (nwg per window)
+  int fs, nbins, M, nwg;
+  size_t nmat() const { return (size_t)W * nbins * nwg; }
 };
 
 static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; return r; }
@@ -789,6 +889,16 @@ static MsmShape make_shape(int n, int c, int W) {
   s.r1 = SegRegion{1 << s.l0, clampG((1 << s.l1) / s.QY), 1 << s.l1};  // Y0 sums
   s.ylanes = (s.r0.count * s.r0.G + s.r1.count * s.r1.G + 63) & ~63;
   s.J = c;
+  {
+    const int lb = c - 1;  // log2 B
+    s.fs = lb > 8 ? lb - 8 : 0;
+    s.nbins = 1 << (lb - s.fs);
+    // ~2048 level-1 workgroups over the pass, at least 2048 entries each
+    size_t M = ((size_t)W * n + 2047) / 2048;
+    M = (M + 255) & ~(size_t)255;
+    s.M = (int)(M < 2048 ? 2048 : M);
+    s.nwg = (int)(((size_t)n + s.M - 1) / s.M);
+  }
   // entries per thread in the level-0 accumulation: 64 at scale (~2^17+ lanes), fewer for
   // small inputs so the serial chain per lane stays short (a lone lane's madd ~12 us)
   {
@@ -808,11 +918,6 @@ constexpr int stitch_bs() { return xyzz_words<F>() > 64 ? 128 : 256; }
 static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.n + s.CH - 1) / s.CH); }
 static size_t stitch_slots1(const MsmShape &s, int bs) { return 2 * ((stitch_slots0(s) + bs - 1) / bs) + 2; }
 
-// bucket sort: LDS counting sort up to c = 16 (one window's histogram, 4 B per bucket,
-// fits LDS), hipCUB radix sort beyond
-constexpr int MSM_LDS_SORT_MAX_C = 16;
-static int bits_for(size_t v) { int b = 1; while (((size_t)1 << b) <= v) b++; return b; }
-
 // sorted entries of one pipeline pass: hipCUB takes int counts, offsets are u32
 constexpr size_t MSM_MAX_GROUP_ENTRIES = (size_t)1 << 30;
 // test hook (zkg_msm_set_group_limit): a smaller cap, so tests reach the multi-group path
@@ -831,17 +936,14 @@ static size_t group_bytes(const MsmShape &s) {
   const size_t maxent = (size_t)s.W * s.n;
   const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s, stitch_bs<F>());
   size_t cub = 0, cub2 = 0;
-  if (s.c <= MSM_LDS_SORT_MAX_C)
-    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(nb + 1)));
-  else
-    ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                (uint32_t *)nullptr, (uint32_t *)nullptr, (int)maxent, 0,
-                                                bits_for(nb)));
+  ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(s.nmat() + 1)));
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)ns0));
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
-  add(maxent * 4 * (s.c <= MSM_LDS_SORT_MAX_C ? 2 : 4));  // list, digits (+ radix sort pairs)
-  add((nb + 1) * 4 * 2);                  // counts / slot cursors, offsets
+  add(maxent * 4 * 3);                    // digits, level-1 values, list
+  add(maxent * 2);                        // level-1 fine indices
+  add((s.nmat() + 1) * 4 * 2);            // level-1 counts, their scan
+  add((nb + 1) * 4);                      // offsets
   add(ns0 * (xw + 4) + ns0 * 16 + 64);    // level-0 items, compacted keys + index, flags, pos, count
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
@@ -915,8 +1017,9 @@ struct GroupPass {
   PhaseProf *prof;
   hipStream_t st;
   size_t nb, xw, maxent, ns0, ns1, cub = 0;
-  bool lds_sort, done = false;
-  uint32_t *list, *dig, *vals, *skeys, *counts, *offsets, *ikeys0, *ivals0, *ckeys, *cidx, *flags, *pos, *ccount;
+  bool done = false;
+  uint32_t *list, *dig, *tmpv, *cnt, *coff, *offsets, *ikeys0, *ivals0, *ckeys, *cidx, *flags, *pos, *ccount;
+  uint16_t *tmpf;
   uint32_t *okA, *ovA, *okB, *ovB, *buckets, *Y, *P0;
   uint64_t *exp;
   void *cubtmp;
@@ -934,12 +1037,12 @@ struct GroupPass {
     xw = xyzz_words<F>();
     maxent = (size_t)s.W * n;
     ZK_REQUIRE(maxent <= MSM_MAX_GROUP_ENTRIES, "msm: window group exceeds the sort capacity (internal sizing bug)");
-    lds_sort = s.c <= MSM_LDS_SORT_MAX_C;
     list = dev.arena.take<uint32_t>(maxent);  // bucket-ordered (point index | sign)
-    dig = dev.arena.take<uint32_t>(maxent);   // digits (LDS sort) / ranks (radix sort)
-    vals = lds_sort ? nullptr : dev.arena.take<uint32_t>(maxent);
-    skeys = lds_sort ? nullptr : dev.arena.take<uint32_t>(maxent);
-    counts = dev.arena.take<uint32_t>(nb + 1);
+    dig = dev.arena.take<uint32_t>(maxent);   // |digit| | sign per (window, point)
+    tmpv = dev.arena.take<uint32_t>(maxent);  // level-1 order: values
+    tmpf = dev.arena.take<uint16_t>(maxent);  // level-1 order: fine bucket within the coarse bin
+    cnt = dev.arena.take<uint32_t>(s.nmat() + 1);
+    coff = dev.arena.take<uint32_t>(s.nmat() + 1);
     offsets = dev.arena.take<uint32_t>(nb + 1);
     ns0 = stitch_slots0(s);
     ns1 = stitch_slots1(s, STITCH_BS);
@@ -959,11 +1062,7 @@ struct GroupPass {
     P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * xw);
     exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
     size_t cub2 = 0;
-    if (lds_sort)
-      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, counts, offsets, (int)(nb + 1), st));
-    else
-      ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, cub, dig, skeys, vals, list, (int)maxent, 0,
-                                                  bits_for(nb), st));
+    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, cnt, coff, (int)(s.nmat() + 1), st));
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
     if (cub2 > cub) cub = cub2;
     cubtmp = dev.arena.take<char>(cub);
@@ -974,41 +1073,23 @@ struct GroupPass {
 
   void sort() {
     const int n = s.n, c = s.c;
-    const int kbits = bits_for(nb);  // radix sort: ranks < nb, zero digits nb
-    if (lds_sort) {
-      hipLaunchKernelGGL((k_digits<C, false>), dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff,
-                         sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig, (uint32_t *)nullptr);
-      ZK_CHECK(hipGetLastError());
-      mark("digits");
-      // M entries per workgroup: at least B (so each workgroup's B bucket atomics stay below
-      // its entry count) and enough workgroups to cover the CUs
-      int M = (int)std::max<size_t>((size_t)s.B, ((size_t)n * s.W + 511) / 512);
-      M = (M + 1023) & ~1023;
-      const dim3 grid(div_up(n, M), s.W);
-      const size_t lds = (size_t)s.B * 4;
-      ZK_CHECK(hipFuncSetAttribute((const void *)k_bucket_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-      ZK_CHECK(hipFuncSetAttribute((const void *)k_bucket_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds));
-      ZK_CHECK(hipMemsetAsync(counts, 0, (nb + 1) * 4, st));
-      hipLaunchKernelGGL(k_bucket_lds<false>, grid, dim3(1024), lds, st, dig, n, M, c, counts, (uint32_t *)nullptr);
-      ZK_CHECK(hipGetLastError());
-      size_t cb = cub;
-      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, counts, offsets, (int)(nb + 1), st));
-      ZK_CHECK(hipMemcpyAsync(counts, offsets, nb * 4, hipMemcpyDeviceToDevice, st));  // slot cursors
-      hipLaunchKernelGGL(k_bucket_lds<true>, grid, dim3(1024), lds, st, dig, n, M, c, counts, list);
-      ZK_CHECK(hipGetLastError());
-    } else {
-      hipLaunchKernelGGL((k_digits<C, true>), dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff,
-                         sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig, vals);
-      ZK_CHECK(hipGetLastError());
-      mark("digits");
-      size_t cb = cub;
-      ZK_CHECK(hipcub::DeviceRadixSort::SortPairs(cubtmp, cb, dig, skeys, vals, list, (int)maxent, 0, kbits, st));
-      hipLaunchKernelGGL(k_offsets_scan, dim3(div_up(maxent, 256)), dim3(256), 0, st, skeys, (uint32_t)maxent,
-                         (uint32_t)nb, offsets);
-      ZK_CHECK(hipGetLastError());
-    }
+    hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff, sc.nread,
+                       sc.mont ? 1 : 0, c, wbase, s.W, dig);
+    ZK_CHECK(hipGetLastError());
+    mark("digits");
+    const dim3 grid((unsigned)s.nwg, (unsigned)s.W);
+    hipLaunchKernelGGL(k_coarse<false>, grid, dim3(256), 0, st, dig, n, s.M, s.fs, s.nbins, cnt, tmpv, tmpf);
+    ZK_CHECK(hipGetLastError());
+    size_t cb = cub;
+    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, cnt, coff, (int)(s.nmat() + 1), st));
+    hipLaunchKernelGGL(k_coarse<true>, grid, dim3(256), 0, st, dig, n, s.M, s.fs, s.nbins, coff, tmpv, tmpf);
+    ZK_CHECK(hipGetLastError());
+    const int cap = fine_stage_cap(s.fs);
+    const int lds = (4 << s.fs) + 4 * cap;
+    ZK_CHECK(hipFuncSetAttribute((const void *)k_fine, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    const uint32_t nq = (uint32_t)(s.W * s.nbins);
+    hipLaunchKernelGGL(k_fine, dim3(nq), dim3(256), lds, st, coff, s.nwg, nq, s.fs, cap, tmpv, tmpf, list, offsets);
+    ZK_CHECK(hipGetLastError());
     mark("sort");
   }
 

@@ -346,6 +346,10 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
   const uint32_t cs = t * (uint32_t)CH;
   const bool active = 2 * t < nslots && cs < total;
   uint32_t k0 = nb, k1 = nb;  // item keys of slots 2t, 2t+1
+  uint32_t tail_b = nb, tail_slot = 0;  // the chunk's right-partial last run (began in the chunk), in acc
+  bool head_end = false;                // slot 2t holds a head run that ends inside the chunk
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
   // gathers the point of list entry `c` (index | sign) into this lane's LDS image
   auto prefetch = [&](uint32_t c) {
     const uint32_t *src = points + (size_t)(c & 0x7fffffffu) * AW;
@@ -372,8 +376,6 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
     uint32_t bbeg = offsets[b], bend = offsets[b + 1];
     uint32_t bnext = offsets[min(b + 2, nb)];  // end of the next bucket, loaded ahead
     bool first_run = true;
-    Xyzz<F> acc;
-    xyzz_set_inf(acc);
     // Flushes store the accumulator LAZILY (X < 14p, Y < 6p for the 381-bit madd): every
     // consumer (xyzz_add / xyzz_dbl / k_export) takes X and Y only into products, which
     // accept those values.  A settle here would cost two products per flush, paid by the
@@ -418,15 +420,47 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
       c1 = c2;
     }
     // last run: partial if it started before the chunk or continues after it
-    if (bbeg < cs || bend > ce) {
-      const uint32_t slot = first_run ? 2 * t : 2 * t + 1;
-      xyzz_store(ivals + (size_t)slot * xyzz_words<F>(), acc);
-      if (first_run) k0 = b; else k1 = b;
+    const bool lpart = bbeg < cs, rpart = bend > ce;
+    if (rpart && !(first_run && lpart)) {  // began in this chunk, continues: kept for the merge below
+      tail_b = b;
+      tail_slot = first_run ? 2 * t : 2 * t + 1;
+    } else if (lpart || rpart) {  // through the whole chunk, or a head that ends exactly at ce
+      xyzz_store(ivals + (size_t)(2 * t) * xyzz_words<F>(), acc);
+      k0 = b;
     } else {
       xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (clamped, unused) gather has landed
+    head_end = k0 != nb && !(first_run && rpart);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last gather and the head flush have landed
   }
+  // Merge across the chunk boundary inside the wavefront: lane t's right-partial last run
+  // and lane t+1's head run (flushed to slot 2t+2 during its loop) are the same bucket's run
+  // exactly when the run crosses that boundary and ends in chunk t+1 -- one add completes
+  // the bucket here instead of two items in the stitch (a run through whole chunks, and the
+  // lane-63 boundary, stay items).  The head is read back at L2 (the other lane's store is
+  // not in this CU's L1).
+  const uint32_t nhead = (uint32_t)__shfl_down((int)(head_end ? k0 : nb), 1, 64);
+  const bool merge = tail_b != nb && lane < 63 && nhead == tail_b;
+  if (__any(merge)) {
+    if (merge) {
+      const uint32_t *src = ivals + (size_t)(2 * t + 2) * xyzz_words<F>();
+      uint32_t wds[xyzz_words<F>()];
+#pragma unroll
+      for (int i = 0; i < xyzz_words<F>(); i++) wds[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      Xyzz<F> o;
+      xyzz_load(o, wds);
+      xyzz_add(acc, o);
+    }
+  }
+  if (tail_b != nb) {
+    if (merge) {
+      xyzz_store(buckets + (size_t)tail_b * xyzz_words<F>(), acc);
+    } else {
+      xyzz_store(ivals + (size_t)tail_slot * xyzz_words<F>(), acc);
+      if (tail_slot == 2 * t) k0 = tail_b; else k1 = tail_b;
+    }
+  }
+  if (__shfl_up((int)merge, 1, 64) && lane > 0) k0 = nb;  // this lane's head went into the lane before
   if (2 * t < nslots) {
     ikeys[2 * t] = k0;
     ikeys[2 * t + 1] = k1;

@@ -259,6 +259,9 @@ ZKG_API void zkg_msm_profile(int on);
 /* test hook: cap on the sorted (window, point) entries one MSM pipeline pass handles
  * (default and maximum 2^30; 0 restores it).  Larger MSMs run in window groups. */
 ZKG_API void zkg_msm_set_group_limit(size_t entries);
+/* test hook: NTT pass split -- 12: two passes of 2^9..2^12-point DFTs (4096-element tiles) for
+ * every 2^17..2^24; 8: passes of <= 2^8-point DFTs only; 0: the default (two passes at 2^20 only) */
+ZKG_API void zkg_ntt_set_max_radix(int r);
 
 /* timing probe of the dominant kernel (MSM bucket accumulation / NTT pass chain),
  * measured with HIP events on each device's own stream; read sums over devices */

@@ -180,3 +180,19 @@ def test_window_groups_vs_oracle(gpu, oracle, curve, window, limit):
     finally:
         gpu.msm_set_group_limit(0)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_repeated_points_linearity(gpu, oracle, curve):
+    """2^16 pairs over 64 distinct points: bucket and Y-sum additions meet equal and opposite
+    partial sums (the doubling / infinity branches of the two-chain Y sums); checked against
+    the oracle and by linearity msm(a + b) = msm(a || b) over the doubled point list"""
+    n = 1 << 16
+    base = gpu.gen_points(curve, 0x5A4B0011, 64)
+    pts = np.ascontiguousarray(np.resize(base, (n, base.shape[1])))
+    a, b = gpu.gen_fr(curve, 702, n), gpu.gen_fr(curve, 703, n)
+    ab = gpu.arr_add(curve, a, b)
+    lhs = gpu.msm_affine(curve, ab, pts)
+    assert np.array_equal(lhs, oracle.msm(curve, ab, pts, mont=True))
+    rhs = gpu.msm_affine(curve, np.concatenate([a, b]), np.concatenate([pts, pts]))
+    assert np.array_equal(lhs, rhs)

@@ -20,9 +20,18 @@ def test_golden(gpu, curve):
         assert np.array_equal(gpu.inverse_ntt(sg, x), i), m
 
 
+@pytest.fixture(params=[0, 12, 8], ids=["default", "two_pass", "short_passes"])
+def radix(gpu, request):
+    """every pass split: the default, two passes of 2^9..2^12-point DFTs on 4096-element tiles
+    for all 2^17..2^24, and <= 2^8-point passes only (test hook zkg_ntt_set_max_radix)"""
+    gpu.ntt_set_max_radix(request.param)
+    yield request.param
+    gpu.ntt_set_max_radix(0)  # default
+
+
 @pytest.mark.parametrize("curve", CURVES)
-@pytest.mark.parametrize("m", [4, 9, 11, 13, 14, 15, 17])
-def test_vs_oracle(gpu, oracle, curve, m):
+@pytest.mark.parametrize("m", [4, 9, 11, 13, 14, 15, 17, 18, 19, 20, 21])
+def test_vs_oracle(gpu, oracle, curve, m, radix):
     sg = gpu.get_fft_subgroup(curve, m)
     x = gpu.gen_fr(curve, 77 + m, 1 << m)
     f = gpu.forward_ntt(sg, x)
@@ -31,7 +40,7 @@ def test_vs_oracle(gpu, oracle, curve, m):
 
 
 @pytest.mark.parametrize("curve", CURVES)
-def test_roundtrip_and_linearity_2_20(gpu, curve):
+def test_roundtrip_and_linearity_2_20(gpu, curve, radix):
     m = 20
     sg = gpu.get_fft_subgroup(curve, m)
     x = gpu.gen_fr(curve, 5, 1 << m)
@@ -49,7 +58,7 @@ def test_config1_bn128_ntt_2_14(gpu):
     assert hashlib.sha256(f.tobytes()).hexdigest() == cfg["forward_sha256"]
 
 
-def test_config3_bls12_381_ntt_2_24(gpu):
+def test_config3_bls12_381_ntt_2_24(gpu, radix):
     cfg = baseline_configs().get("config3_bls12_381_ntt_2^24")
     if cfg is None:
         pytest.skip("baseline_configs.json missing config3")

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Device-resident NTT timing for A/B runs on the GPU box (ZK_LIB_PATH selects a build):
-   python tools/ntt_time.py [log_n] [reps]
+   python tools/ntt_time.py [log_n] [reps] [max_radix]   (max_radix 12: two-pass schedule, 8: three passes)
 Prints forward / inverse ms per transform, the forward output's SHA-256 against the
 reference digest at 2^24 (tests/golden/baseline_configs.json) and the round-trip check."""
 import hashlib
@@ -16,6 +16,8 @@ import zkalgebra as zk  # noqa: E402
 
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 24
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+if len(sys.argv) > 3:
+    zk.ntt_set_max_radix(int(sys.argv[3]))
 curve = "bls12_381"
 n = 1 << m
 x = zk.gen_fr(curve, 0x5A4B0003, n)
@@ -23,7 +25,7 @@ g = zk.get_fft_subgroup(curve, m).gen_array()
 d_x, d_f, d_i = zk.DeviceBuffer(x), zk.DeviceBuffer.empty(x.nbytes), zk.DeviceBuffer.empty(x.nbytes)
 zk.ntt_device(curve, m, g, d_x, d_f)
 zk.ntt_device(curve, m, g, d_f, d_i, inverse=True)
-out = {}
+out = {"m": m, "max_radix": int(sys.argv[3]) if len(sys.argv) > 3 else 12}
 for name, src, dst, inv in (("fwd", d_x, d_f, False), ("inv", d_f, d_i, True)):
     zk.load().zkg_device_synchronize()
     zk.timer(enable=True, reset=True)

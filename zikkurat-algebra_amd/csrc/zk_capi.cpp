@@ -275,6 +275,7 @@ ZKG_API int zkg_msm_default_window(int npoints) { return zk::msm_default_window(
 
 ZKG_API void zkg_msm_profile(int on) { zk::msm_set_profile(on); }
 ZKG_API void zkg_msm_set_group_limit(size_t entries) { zk::msm_set_group_limit(entries); }
+ZKG_API void zkg_ntt_set_max_radix(int r) { zk::ntt_set_max_radix(r); }
 
 ZKG_API double zkg_field_mul_rate(int field) { return zk::field_mul_rate(field); }
 

@@ -17,6 +17,7 @@
 // output straight to its natural index k = sum_q k_q T_q (no bit-reversal pass).
 // Inverse: w -> w^-1 and the 1/N factor folded into pass 0's twiddle table.
 // Twiddle tables are built on the device once per (curve, m, gen, direction) and cached.
+#include <atomic>
 #include <map>
 #include <tuple>
 #include <vector>
@@ -27,8 +28,13 @@
 
 namespace zk {
 
+// Two pass-kernel widths: 256 threads over 1024-element tiles (36 KB of LDS, 4 workgroups
+// per CU) for DFTs of up to 2^8 points, and 1024 threads over 4096-element tiles (144 KB: one
+// workgroup per CU) for the 2^9..2^12-point DFTs of the two-pass schedule (2^17..2^24).
 constexpr int NTT_THREADS = 256;
 constexpr int NTT_TILE = 1024;  // elements per workgroup tile for multi-pass transforms
+constexpr int NTT_THREADS_BIG = 1024;
+constexpr int NTT_TILE_BIG = 4096;
 // Inner twiddles are read from a global (L1/L2-resident, a few KB) internal-limb table with
 // 48-B rows (3 x 16-B loads) rather than staged in LDS: the 1024-element tile alone is
 // 36 KB, so dropping the 4.6 KB twiddle copy lets 4 instead of 3 workgroups share a CU.
@@ -114,15 +120,17 @@ __global__ void k_tw_inner_int(uint32_t *__restrict__ itw_i, const uint64_t *__r
 
 // ---------------------------------------------------------------------------- pass kernel
 
-// LDS slot of tile element I: an XOR swizzle of the low 6 index bits by bits 6..9, so that
+// LDS slot of tile element I: an XOR swizzle of the low 6 index bits by bits 6..11, so that
 // every access pattern of the pass (bit-reversed loads, the radix-4 rounds at every stride,
-// G-interleaved stores) hits 64 distinct banks with 9-word elements (verified by brute
-// force over the tile shapes; the plain layout had 4-16-way conflicts: rocprofv3
-// SQ_LDS_BANK_CONFLICT was 80 % of the LDS-active cycles, profiles/r02o_ntt_lds.txt)
+// G-interleaved stores) hits 64 distinct banks with 9-word elements, for the 1024-element
+// tiles (R = 2^8, G = 4) and every 4096-element tile shape (R = 2^9..2^12) -- checked by brute
+// force over the wave access patterns (tools/ntt_lds_banks.py); the plain layout had 4-16-way
+// conflicts (rocprofv3 SQ_LDS_BANK_CONFLICT was 80 % of the LDS-active cycles,
+// profiles/r02o_ntt_lds.txt)
 __device__ __forceinline__ uint32_t lds_slot(uint32_t I) {
-  const uint32_t m1 = (I >> 6) & 3, m2 = (I >> 8) & 3;
-  const uint32_t x = m1 ^ m2;
-  return I ^ (m1 | (x << 2) | (x << 4));
+  const uint32_t m1 = (I >> 6) & 3, m2 = (I >> 8) & 3, m3 = (I >> 10) & 3;
+  const uint32_t x = m1 ^ m2, y = x ^ m3;
+  return I ^ (m1 | (x << 2) | (y << 4));
 }
 
 template <class F>
@@ -143,7 +151,7 @@ __device__ __forceinline__ void lds_put(uint32_t *p, const Fe<F> &x) {
 // values are < 33p, well inside fe_mul's input range (R'/p > 140): the products of the
 // next stage and the pass's closing product (twiddle / scale / one) bring them back
 // below 2p.  Limb bound: normalised (< 2^29) at round entry, < 2^31.4 at round exit.
-template <class F>
+template <class F, int NT>
 __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restrict__ itw, int r, int G) {
   constexpr int NW = F::N;
   const int R = 1 << r;
@@ -153,7 +161,7 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
     const int q4 = R >> 2;
     Fe<F> w3;
     lds_get(w3, itw + (size_t)(R / 4) * ITW_STRIDE);  // w_4 = w_R^(R/4)
-    for (int u = tid; u < G * q4; u += NTT_THREADS) {
+    for (int u = tid; u < G * q4; u += NT) {
       const int g = u / q4, j = u % q4;
       const int i0 = g * R + j * 4;
       Fe<F> a0, a1, a2, a3, b0, b1, b3, t;
@@ -186,7 +194,7 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
   for (; s + 1 < r; s += 2) {  // radix-4 rounds: stages s and s+1
     const int half = 1 << s;
     const int q4 = R >> 2;
-    for (int u = tid; u < G * q4; u += NTT_THREADS) {
+    for (int u = tid; u < G * q4; u += NT) {
       const int g = u / q4, j = u % q4;
       const int blk = j >> s, off = j & (half - 1);
       const int i0 = g * R + blk * 4 * half + off;
@@ -227,7 +235,7 @@ __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restri
   if (s < r) {  // odd r: one radix-2 stage left
     const int half = 1 << s;
     const int q2 = R >> 1;
-    for (int u = tid; u < G * q2; u += NTT_THREADS) {
+    for (int u = tid; u < G * q2; u += NT) {
       const int g = u / q2, j = u % q2;
       const int blk = j >> s, off = j & (half - 1);
       const int i0 = g * R + blk * 2 * half + off;
@@ -268,8 +276,8 @@ struct PassArgs {
 //                  tile = G consecutive lo for one hi; output * tab[k*S + lo]
 //   last pass    : S == 1; instance = position prefix (k_0..k_{P-2}); element k at inst*R + k;
 //                  tile = G instances with consecutive k_0; output to natural index
-template <class F>
-__global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__restrict__ src, uint64_t *__restrict__ dst,
+template <class F, int NT>
+__global__ void __launch_bounds__(NT) k_ntt_pass(const uint64_t *__restrict__ src, uint64_t *__restrict__ dst,
                                                           PassArgs a, const uint32_t *__restrict__ itw_i,
                                                           const uint64_t *__restrict__ tab,
                                                           const uint64_t *__restrict__ scale,
@@ -314,7 +322,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
 
   // load: element (g, k) -> LDS slot g*R + bitrev_r(k)
   const int nel = G * R;
-  for (int e = tid; e < nel; e += NTT_THREADS) {
+  for (int e = tid; e < nel; e += NT) {
     int g, k;
     size_t addr;
     if (!a.last) {
@@ -334,7 +342,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
   }
   __syncthreads();
 
-  lds_dft<F>(data, itw, r, G);
+  lds_dft<F, NT>(data, itw, r, G);
 
   Fe<F> sc;
   if (scale) {
@@ -344,7 +352,7 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
   } else {
     fe_one(sc);
   }
-  for (int e = tid; e < nel; e += NTT_THREADS) {
+  for (int e = tid; e < nel; e += NT) {
     const int g = e % G, k = e / G;  // consecutive threads -> consecutive g (coalesced)
     Fe<F> x;
     lds_get(x, data + (size_t)lds_slot((uint32_t)(g * R + k)) * NW);
@@ -375,12 +383,29 @@ __global__ void __launch_bounds__(NTT_THREADS) k_ntt_pass(const uint64_t *__rest
 
 // ---------------------------------------------------------------------------- host side
 
+// Pass split.  Default: three-or-more passes of <= 2^8-point DFTs on 1024-element tiles,
+// except 2^20 = 2^10 x 2^10, which runs as two passes on 4096-element tiles (G = 4 columns:
+// 128-B row segments, 256 tiles per pass): 0.128 vs 0.144 ms (profiles/r02am_ntt_two_pass.txt).
+// Two passes lose elsewhere: below 2^20 a pass has fewer than 256 tiles (2^18: 0.101 vs
+// 0.057 ms), above it the column pass gets G <= 2 columns, i.e. 32- or 64-B row segments
+// (2^22: 0.575 vs 0.556 ms; 2^24 = 2^12 x 2^12: 2.65 vs 2.09 ms, 2.42 ms with the 4 workgroups
+// sharing each 128-B line placed on one XCD).  Test hook zkg_ntt_set_max_radix: 12 forces the
+// two-pass split for every 2^17..2^24, 8 forbids it, 0 restores the default.
+static std::atomic<int> g_ntt_max_radix{0};
+void ntt_set_max_radix(int r) { g_ntt_max_radix.store(r == 8 || r == 12 ? r : 0); }
+
 static void split_digits(int m, std::vector<int> &d) {
   d.clear();
   if (m == 0) { d.push_back(0); return; }
-  int P = (m + 7) / 8;
-  if (m <= 11) P = 1;  // one workgroup-sized DFT
-  int base = m / P, extra = m % P;
+  if (m <= 11) { d.push_back(m); return; }  // one workgroup-sized DFT
+  const int mode = g_ntt_max_radix.load();
+  if ((mode == 12 && m >= 17 && m <= 24) || (mode == 0 && m == 20)) {  // two passes, 2^9..2^12 points each
+    d.push_back((m + 1) / 2);
+    d.push_back(m / 2);
+    return;
+  }
+  const int P = (m + 7) / 8;
+  const int base = m / P, extra = m % P;
   for (int p = 0; p < P; p++) d.push_back(base + (p < extra ? 1 : 0));
 }
 
@@ -407,7 +432,8 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
                        const std::vector<int> &dig) {
   using F = typename Cfg::Fd;
   using HF = typename Cfg::Fh;
-  TwKey key(dev.id * 2 + curve, m, inverse, gen_mont[0], gen_mont[1], gen_mont[2], gen_mont[3]);
+  // the tables depend on the pass split too (the test hook can change it between calls)
+  TwKey key(dev.id * 2 + curve, m | (dig[0] << 8), inverse, gen_mont[0], gen_mont[1], gen_mont[2], gen_mont[3]);
   std::lock_guard<std::mutex> lock(g_tw_mu);
   auto it = g_tw.find(key);
   if (it != g_tw.end()) {
@@ -567,14 +593,16 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     S >>= r;
     const int last = (p == P - 1);
     uint64_t *out = last ? d_dst : scratch;
+    const bool big = r > 8;  // 2^9..2^12-point DFTs: 1024 threads over 4096-element tiles
+    const int tile = big ? NTT_TILE_BIG : NTT_TILE;
     int G;
     if (P == 1) {
       G = 1;
     } else if (!last) {
-      G = NTT_TILE / R;
+      G = tile / R;
       if ((size_t)G > S) G = (int)S;
     } else {
-      G = NTT_TILE / R;
+      G = tile / R;
       if (G > (1 << dig[0])) G = 1 << dig[0];
     }
     const size_t ntiles = N / ((size_t)R * G);
@@ -586,10 +614,15 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     pa.G = G;
     pa.h = tw.h;
     pa.otf = (!last && !tw.tab[p]) ? 1 : 0;
-    ZK_CHECK(hipFuncSetAttribute((const void *)k_ntt_pass<F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const void *kfn = big ? (const void *)k_ntt_pass<F, NTT_THREADS_BIG> : (const void *)k_ntt_pass<F, NTT_THREADS>;
+    ZK_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     if (p == 0) timer_begin(dev);
-    hipLaunchKernelGGL(k_ntt_pass<F>, dim3((unsigned)ntiles), dim3(NTT_THREADS), lds, st, in, out, pa, tw.inner_i[p],
-                       tw.tab[p], last ? tw.scale : nullptr, tw.tlo, tw.thi);
+    if (big)
+      hipLaunchKernelGGL((k_ntt_pass<F, NTT_THREADS_BIG>), dim3((unsigned)ntiles), dim3(NTT_THREADS_BIG), lds, st, in,
+                         out, pa, tw.inner_i[p], tw.tab[p], last ? tw.scale : nullptr, tw.tlo, tw.thi);
+    else
+      hipLaunchKernelGGL((k_ntt_pass<F, NTT_THREADS>), dim3((unsigned)ntiles), dim3(NTT_THREADS), lds, st, in, out,
+                         pa, tw.inner_i[p], tw.tab[p], last ? tw.scale : nullptr, tw.tlo, tw.thi);
     ZK_CHECK(hipGetLastError());
     if (last) timer_end(dev);
     in = out;

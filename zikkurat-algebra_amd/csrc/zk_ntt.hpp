@@ -7,4 +7,7 @@ namespace zk {
 // when host_io, device pointers otherwise.  inverse: interpolation incl. the 1/N factor.
 void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst, bool host_io,
          bool inverse);
+// test hook: pass split, 12 (two passes for every 2^17..2^24), 8 (<= 2^8-point passes only) or
+// 0 (default: two passes at 2^20 only)
+void ntt_set_max_radix(int r);
 }  // namespace zk

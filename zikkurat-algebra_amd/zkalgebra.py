@@ -59,7 +59,7 @@ EXTENSION_SYMBOLS = [
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
     "zkg_field_mul_rate", "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
     "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
-    "zkg_msm_profile", "zkg_msm_set_group_limit",
+    "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_ntt_set_max_radix",
 ]
 
 _lib = None
@@ -536,6 +536,11 @@ def msm_profile(on):
 def msm_set_group_limit(entries):
     """test hook: max sorted entries per MSM pipeline pass (0 = default 2^30)"""
     load().zkg_msm_set_group_limit(int(entries))
+
+
+def ntt_set_max_radix(r):
+    """test hook: NTT pass split -- 12: two passes for 2^17..2^24, 8: <= 2^8-point passes, 0: default"""
+    load().zkg_ntt_set_max_radix(int(r))
 
 
 def arr_op_device(curve, op, n, d_a, d_b=None, d_c=None, kA=None, kB=None, d_tgt=None):

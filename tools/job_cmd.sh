@@ -1,4 +1,8 @@
 # scratch commands of the current GPU experiment (run by tools/gpu_job.sh step "cmd")
-export ZK_LIB_PATH=$PWD/variants/onechain/libzkalgebra_gpu.so
-timeout 300 python -u -m pytest tests/test_gpu_msm.py -q -x --timeout 120 --timeout-method thread 2>&1 | tail -3
-timeout 300 python -u tools/sweep_window.py phases
+# two-chain Y sums with interleaved product pairs (variants/ilv) vs the in-tree build
+ZK_LIB_PATH=$PWD/variants/ilv/libzkalgebra_gpu.so timeout 300 python -u -m pytest tests/test_gpu_msm.py -q -x --timeout 120 --timeout-method thread 2>&1 | tail -2
+for v in base ilv base ilv; do
+  if [ $v = base ]; then export ZK_LIB_PATH=; else export ZK_LIB_PATH=$PWD/variants/$v/libzkalgebra_gpu.so; fi
+  echo "== $v"
+  timeout 100 python tools/sweep_window.py phases2 2>&1 | grep -E "ms/msm|^\[zk msm\]" | awk 'NR%5==0 || /ms\/msm/'
+done

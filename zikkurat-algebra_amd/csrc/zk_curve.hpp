@@ -188,11 +188,57 @@ __device__ __forceinline__ void xyzz_add_aff_lazy(Xyzz<F> &acc, const Aff<F> &a)
   fe_mul(acc.ZZ, acc.ZZ, PP);
   fe_mul(acc.ZZZ, acc.ZZZ, PPP);
 }
-// dispatch: lazy variant for the 381-bit field, exact variant otherwise (the 254-bit
-// fields have only 3 spare bits per limb and R'/p ~ 2^7.4: not enough for these bounds)
+// The same for the 254-bit base field (9 x 29-bit limbs, R'/p ~ 2^7.4: too little headroom to
+// keep X lazily, so X3 is brought below 2p by the product-free fe_reduce_small).  The
+// accumulator keeps the exact invariant X, Y, ZZ, ZZZ < 2p, normalised.  Bounds (values in
+// units of p; checked for BN254 by tools/lazy_bounds.py):
+//   P = U2 + 3p - X1 < 5p,  R = S2 + 3p - Y1 < 5p        (normalised before squaring)
+//   X3 = RR + 3p - PPP + 5p - 2Q < 10p -> fe_reduce_small -> < 2p
+//   Y3 = (R (Q + 3p - X3) + (3p - Y1) PPP) / R' :  (25 + 6) p^2 < p R'  ->  Y3 < 2p
+// Limbs: every product operand is normalised (< 2^29; top limbs < 2^25), so fe_mul2's
+// column sums stay below 27 * 2^58 < 2^63.
+template <class F>
+__device__ __forceinline__ void xyzz_add_aff_lazy9(Xyzz<F> &acc, const Aff<F> &a) {
+  static_assert(F::N == 9 && F::RB == 29, "bounds derived for the 9 x 29-bit fields");
+  if (xyzz_is_inf(acc)) { xyzz_from_aff(acc, a); return; }
+  Fe<F> P, R, PP, RR, t;
+  fe_mul(t, a.x, acc.ZZ);                 // U2
+  fe_sub_lazy<F, 3, 1>(P, t, acc.X);      // P = U2 - X1
+  fe_norm(P);
+  fe_mul(t, a.y, acc.ZZZ);                // S2
+  fe_sub_lazy<F, 3, 1>(R, t, acc.Y);      // R = S2 - Y1
+  fe_norm(R);
+  fe_sqr(PP, P);
+  fe_sqr(RR, R);
+  if (fe_is_zero(PP)) {
+    if (fe_is_zero(RR)) { xyzz_dbl_aff(acc, a); }
+    else { xyzz_set_inf(acc); }
+    return;
+  }
+  Fe<F> PPP, Q, X3, q2;
+  fe_mul(PPP, P, PP);
+  fe_mul(Q, acc.X, PP);
+  fe_sub_lazy<F, 3, 1>(t, RR, PPP);       // RR - PPP
+  fe_add_lazy(q2, Q, Q);
+  fe_sub_lazy<F, 5, 2>(X3, t, q2);        // - 2Q
+  fe_norm(X3);
+  fe_reduce_small(X3);                    // < 2p
+  fe_sub_lazy<F, 3, 1>(t, Q, X3);         // Q - X3
+  fe_norm(t);
+  Fe<F> ny;
+  fe_sub_lazy<F, 3, 1>(ny, Fe<F>{}, acc.Y);  // 3p - Y1
+  fe_norm(ny);
+  fe_mul2(acc.Y, R, t, ny, PPP);          // Y3 = R (Q - X3) - Y1 PPP
+  acc.X = X3;
+  fe_mul(acc.ZZ, acc.ZZ, PP);
+  fe_mul(acc.ZZZ, acc.ZZZ, PPP);
+}
+
+// dispatch: lazy variants for the 381-bit and the 254-bit base fields, exact otherwise (Fp2)
 template <class F>
 __device__ __forceinline__ void xyzz_acc_aff(Xyzz<F> &acc, const Aff<F> &a) {
   if constexpr (F::N == 14) xyzz_add_aff_lazy(acc, a);
+  else if constexpr (F::N == 9 && F::RB == 29) xyzz_add_aff_lazy9(acc, a);
   else xyzz_add_aff(acc, a);
 }
 

@@ -319,7 +319,7 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ offse
 //
 //    The next entry's point is gathered straight into LDS by global_load_lds (16 B per lane
 //    per instruction, lane-linear image [chunk][lane][16 B] per wave) while the current
-//    mixed add runs, so the prefetch costs no VGPRs (the 254-bit madd fits 4 waves per SIMD;
+//    mixed add runs, so the prefetch costs no VGPRs (the 254-bit madd fits 3 waves per SIMD;
 //    the 381-bit one stays at 2: forced to 3 it spills ~56 VGPRs inside the loop, measured
 //    3.12 vs 2.56 ms at 2^20).
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -327,7 +327,9 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 
 template <class F>
 struct AccumOcc {  // minimum waves per SIMD k_accum is compiled for
-  static constexpr int waves = F::N >= 28 ? 1 : (F::N >= 14 ? 2 : 4);
+  // 254-bit lazy madd: 3 waves (153 VGPRs); at 4 it spills 30 VGPRs inside the loop (1.49 vs
+  // 1.44 ms at BN128 2^20, profiles/r02at_bn128_lazy_madd.txt)
+  static constexpr int waves = F::N >= 28 ? 1 : (F::N >= 14 ? 2 : 3);
 };
 
 template <class C>

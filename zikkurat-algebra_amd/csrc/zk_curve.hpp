@@ -278,6 +278,69 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
   fe_mul(acc.ZZZ, acc.ZZZ, PPP);
 }
 
+// acc += b (add-2008-s) for the G1 reductions (Y sums), with lazy differences and the shared-
+// reduction Y3 of the lazy mixed adds above.  Inputs in the bucket forms (381-bit: X < 14p,
+// Y < 6p; 254-bit: X, Y < 2p), output in the same form (Y3 < 2p).  Bounds, in units of p:
+//   381-bit: P = U2 + 4p - U1 < 6p, R = S2 + 4p - S1 < 6p, X3 < 14p as in the madd,
+//            Y3: R (Q + 16p - X3) + (4p - S1) PPP < (6 * 18 + 4 * 2) p^2 < p R' (R'/p > 2^11)
+//   254-bit: as xyzz_add_aff_lazy9 with U1, S1 (< 2p) in place of X1, Y1
+template <class F>
+__device__ __forceinline__ void xyzz_add_lazy(Xyzz<F> &acc, const Xyzz<F> &b) {
+  static_assert(F::N == 14 || (F::N == 9 && F::RB == 29), "lazy bounds derived for the G1 base fields");
+  constexpr bool W9 = F::N == 9;
+  if (xyzz_is_inf(b)) return;
+  if (xyzz_is_inf(acc)) { acc = b; return; }
+  Fe<F> U1, S1, P, R, PP, RR, t;
+  fe_mul(U1, acc.X, b.ZZ);
+  fe_mul(t, b.X, acc.ZZ);                             // U2
+  if constexpr (W9) { fe_sub_lazy<F, 3, 1>(P, t, U1); fe_norm(P); }
+  else fe_sub_lazy<F, 4, 1>(P, t, U1);                // P = U2 - U1
+  fe_mul(S1, acc.Y, b.ZZZ);
+  fe_mul(t, b.Y, acc.ZZZ);                            // S2
+  if constexpr (W9) { fe_sub_lazy<F, 3, 1>(R, t, S1); fe_norm(R); }
+  else fe_sub_lazy<F, 4, 1>(R, t, S1);                // R = S2 - S1
+  fe_sqr(PP, P);
+  fe_sqr(RR, R);
+  if (fe_is_zero(PP)) {
+    if (fe_is_zero(RR)) { xyzz_dbl(acc, b); }
+    else { xyzz_set_inf(acc); }
+    return;
+  }
+  Fe<F> PPP, Q, X3, q2, ny;
+  fe_mul(PPP, P, PP);
+  fe_mul(Q, U1, PP);
+  fe_add_lazy(q2, Q, Q);
+  if constexpr (W9) {
+    fe_sub_lazy<F, 3, 1>(t, RR, PPP);
+    fe_sub_lazy<F, 5, 2>(X3, t, q2);                  // RR - PPP - 2Q < 10p
+    fe_norm(X3);
+    fe_reduce_small(X3);                              // < 2p
+    fe_sub_lazy<F, 3, 1>(t, Q, X3);
+    fe_norm(t);
+    fe_sub_lazy<F, 3, 1>(ny, Fe<F>{}, S1);
+    fe_norm(ny);
+  } else {
+    fe_sub_lazy<F, 4, 1>(t, RR, PPP);
+    fe_sub_lazy<F, 8, 2>(X3, t, q2);                  // RR - PPP - 2Q < 14p
+    fe_norm(X3);
+    fe_sub_lazy<F, 16, 1>(t, Q, X3);                  // Q - X3 < 18p
+    fe_sub_lazy<F, 4, 1>(ny, Fe<F>{}, S1);            // 4p - S1
+  }
+  Fe<F> zz, zzz;
+  fe_mul(zz, acc.ZZ, b.ZZ);
+  fe_mul(zzz, acc.ZZZ, b.ZZZ);
+  fe_mul2(acc.Y, R, t, ny, PPP);                      // Y3 = R (Q - X3) - S1 PPP
+  acc.X = X3;
+  fe_mul(acc.ZZ, zz, PP);
+  fe_mul(acc.ZZZ, zzz, PPP);
+}
+// the Y sums' addition: lazy for the G1 base fields, exact for Fp2
+template <class F>
+__device__ __forceinline__ void xyzz_add_red(Xyzz<F> &acc, const Xyzz<F> &b) {
+  if constexpr (F::N == 14 || (F::N == 9 && F::RB == 29)) xyzz_add_lazy(acc, b);
+  else xyzz_add(acc, b);
+}
+
 // Affine points on the device are kept in INTERNAL form (converted once per call by
 // k_points_int): 2 x SN u32 words; the reference's all-0xFF infinity sentinel becomes a
 // first word of 0xFFFFFFFF (never a valid limb).  Returns false for infinity.

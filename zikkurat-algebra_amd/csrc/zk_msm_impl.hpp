@@ -524,7 +524,7 @@ __global__ void __launch_bounds__(BS) k_stitch_blk(const uint32_t *__restrict__ 
     if (need) {
       Xyzz<F> o;
       xyzz_load(o, lv + (size_t)(t - d) * XW);
-      xyzz_add(acc, o);
+      xyzz_add_red(acc, o);
     }
     __syncthreads();
   }
@@ -696,7 +696,7 @@ __global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buck
     }
     if (full) {
       if (!PF) xyzz_load(cur, wb + (size_t)mc * XW);
-      xyzz_add(acc, cur);
+      xyzz_add_red(acc, cur);
     }
   }
   for (int h = 128; h >= S; h >>= 1) {
@@ -705,7 +705,7 @@ __global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buck
     if (t < h) {
       Xyzz<F> o;
       xyzz_load(o, park + (size_t)t * XW);
-      xyzz_add(acc, o);
+      xyzz_add_red(acc, o);
     }
     __syncthreads();
   }

@@ -1203,7 +1203,7 @@ struct GroupPass {
   // Only when level 2 still left more than one chunk of items (skewed scalars) does the
   // host run further levels and redo the tail.
   void finish() {
-    ZK_CHECK(hipStreamSynchronize(st));
+    stream_wait(dev, st);
     if (!done && *hc > (uint32_t)STITCH_BS) {
       for (;;) {
         if (stitch_level()) break;

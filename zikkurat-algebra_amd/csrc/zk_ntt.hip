@@ -629,7 +629,7 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     T <<= r;
   }
   if (host_io) ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
-  ZK_CHECK(hipStreamSynchronize(st));
+  stream_wait(dev, st);
   timer_collect(dev);
 }
 

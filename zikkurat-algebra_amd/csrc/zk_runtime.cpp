@@ -51,6 +51,16 @@ Device &current_device() {
   return *g_devices[id];
 }
 
+void stream_wait(Device &dev, hipStream_t st) {
+  if (!dev.sync_ev) ZK_CHECK(hipEventCreateWithFlags(&dev.sync_ev, hipEventDisableTiming));
+  ZK_CHECK(hipEventRecord(dev.sync_ev, st));
+  for (;;) {
+    const hipError_t e = hipEventQuery(dev.sync_ev);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) ZK_CHECK(e);
+  }
+}
+
 // ---------------------------------------------------------------------------- kernel timer
 static std::atomic<bool> g_timer_on{false};
 

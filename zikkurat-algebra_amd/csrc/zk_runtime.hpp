@@ -76,7 +76,13 @@ struct Device {
   size_t pinned_cap = 0;
   void *host_staging(size_t bytes);
   KernelTimer timer;
+  hipEvent_t sync_ev = nullptr;  // stream_wait's marker
 };
+
+// Wait for everything enqueued on st by spinning on an event (caller holds dev.mu): the
+// synchronous entry points return as soon as the GPU is done, without the wake-up latency of
+// a blocking stream synchronisation (up to ~0.1 ms measured in the MSM's export phase).
+void stream_wait(Device &dev, hipStream_t st);
 
 // The device of the calling thread (hipGetDevice), lazily initialised.
 Device &current_device();

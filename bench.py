@@ -27,6 +27,7 @@ import glob
 import hashlib
 import json
 import os
+import re
 import sys
 import time
 
@@ -70,9 +71,18 @@ def baseline():
     return json.load(open(p)) if os.path.exists(p) else {}
 
 
+def profile_order(path):
+    """sort key of a profile file name rNN<tag>_...: round, then the tag in the order tags are
+    issued (a..z, then aa..az, ...), so r02e < r02au (plain string order would put r02e last)"""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    if not m:
+        return (-1, 0, "", path)
+    return (int(m.group(1)), len(m.group(2)), m.group(2), path)
+
+
 def latest_profile(pattern):
     """newest committed profile file matching profiles/<pattern> (file names carry the round)"""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=profile_order)
     if not files:
         return None, None
     try:
@@ -84,7 +94,7 @@ def latest_profile(pattern):
 def load_pmc(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*pmc*.json)"""
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=profile_order):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):

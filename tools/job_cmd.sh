@@ -1,11 +1,19 @@
 # scratch commands of the current GPU experiment (run by tools/gpu_job.sh step "cmd")
-# event spin-wait at the end of the synchronous MSM / NTT calls (in-tree) vs blocking stream sync (variants/prev)
-timeout 300 python -u -m pytest tests/test_gpu_msm.py tests/test_gpu_ntt.py tests/test_gpu_concurrency.py -q -x --timeout 120 --timeout-method thread 2>&1 | tail -2
-for v in prev new prev new; do
+# point conversion on a second stream beside the sort (in-tree) vs one stream (variants/prev), 20 reps, alternating
+cat > /tmp/ab.py <<'PY'
+import sys, time, os
+sys.path.insert(0, os.path.join(os.environ["GRAFT_REPO_ROOT"], "zikkurat-algebra_amd"))
+import zkalgebra as zk
+for curve, logn in (("bls12_381", 20), ("bls12_381", 16), ("bn128", 20)):
+    n = 1 << logn
+    ds, dp = zk.DeviceBuffer(zk.gen_fr(curve, 0x5A4B0002, n)), zk.DeviceBuffer(zk.gen_points(curve, 0x5A4B0002, n))
+    for _ in range(3): zk.msm_device(curve, n, ds, dp)
+    t = time.perf_counter()
+    for _ in range(20): zk.msm_device(curve, n, ds, dp)
+    print(curve, logn, round((time.perf_counter() - t) / 20 * 1e3, 4), "ms", flush=True)
+    ds.free(); dp.free()
+PY
+for v in prev new prev new prev new; do
   if [ $v = new ]; then export ZK_LIB_PATH=; else export ZK_LIB_PATH=$PWD/variants/$v/libzkalgebra_gpu.so; fi
-  echo "== $v"
-  timeout 100 python tools/sweep_window.py bls12_381 20
-  timeout 100 python tools/sweep_window.py bls12_381 16
-  timeout 100 python tools/sweep_window.py bn128 20
-  timeout 100 python tools/ntt_time.py 24 20
+  echo "== $v"; timeout 120 python /tmp/ab.py
 done

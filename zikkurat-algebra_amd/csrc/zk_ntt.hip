@@ -133,6 +133,16 @@ __device__ __forceinline__ uint32_t lds_slot(uint32_t I) {
   return I ^ (m1 | (x << 2) | (y << 4));
 }
 
+// value < 2^(64 N64) with normalised limbs -> N64 u64 words, as is (no canonicalisation)
+template <class F>
+__device__ __forceinline__ void fe_store_packed(uint64_t *__restrict__ p, const Fe<F> &a) {
+  uint32_t w[F::NW];
+  fe_pack(w, a);
+  uint4 *q = reinterpret_cast<uint4 *>(p);
+#pragma unroll
+  for (int i = 0; i < F::NW / 4; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
 template <class F>
 __device__ __forceinline__ void lds_get(Fe<F> &x, const uint32_t *p) {
 #pragma unroll
@@ -147,10 +157,11 @@ __device__ __forceinline__ void lds_put(uint32_t *p, const Fe<F> &x) {
 // in-LDS DIT over G instances of R points (bit-reversed input order -> natural order).
 // Lazy butterflies (zk_field.hpp "lazy ops"): x = a + t, y = a + 4p - t with no carries
 // or reductions; limbs are renormalised once per radix-4 round when written back to LDS.
-// Value bound: inputs < p, every stage adds < 4p, so after R = 2^8 points (8 stages)
-// values are < 33p, well inside fe_mul's input range (R'/p > 140): the products of the
-// next stage and the pass's closing product (twiddle / scale / one) bring them back
-// below 2p.  Limb bound: normalised (< 2^29) at round entry, < 2^31.4 at round exit.
+// Value bound: inputs < 2p (canonical input, or the previous pass's product output), every
+// stage adds < 4p, so after R = 2^8 points (8 stages) values are < 34p, well inside fe_mul's
+// input range (R'/p > 68) and fe_reduce_small's (< 64p): the products of the next stage and
+// the pass's closing product (twiddle / scale) or reduction bring them back below 2p.  (The
+// 4096-point tiles add 12 stages: < 50p.)  Limb bound: normalised (< 2^29) at round entry, < 2^31.4 at round exit.
 template <class F, int NT>
 __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restrict__ itw, int r, int G) {
   constexpr int NW = F::N;
@@ -377,7 +388,10 @@ __global__ void __launch_bounds__(NT) k_ntt_pass(const uint64_t *__restrict__ sr
         fe_reduce_small(x);
       }
     }
-    fe_store_ref(dst + addr * F::N64, x);
+    // a non-last pass's output is a product (< 2p < 2^256, both Fr moduli are below 2^255):
+    // stored packed but not canonicalised -- the next pass only multiplies and adds it
+    if (!a.last) fe_store_packed(dst + addr * F::N64, x);
+    else fe_store_ref(dst + addr * F::N64, x);
   }
 }
 

@@ -379,7 +379,7 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
     uint32_t bnext = offsets[min(b + 2, nb)];  // end of the next bucket, loaded ahead
     bool first_run = true;
     // Flushes store the accumulator LAZILY (X < 14p, Y < 6p for the 381-bit madd): every
-    // consumer (xyzz_add / xyzz_dbl / k_export) takes X and Y only into products, which
+    // consumer (xyzz_add / xyzz_dbl / the job sums' export) takes X and Y only into products, which
     // accept those values.  A settle here would cost two products per flush, paid by the
     // whole wavefront whenever any lane flushes (runs average 32 entries at 2^20).
     // Pipeline: the point of entry e+1 lands in LDS and the list index of entry e+2 in a
@@ -821,7 +821,7 @@ __device__ __forceinline__ void xyzz_add_quad(Xyzz<F> &acc, const Xyzz<F> &b, ui
 //    fold inside one wavefront (16 quads) would leave 8-16 items serial per quad.
 template <class C>
 __global__ void __launch_bounds__(256) k_jobsum_blk(const uint32_t *__restrict__ Y, int c, int l0,
-                                                    uint32_t *__restrict__ out) {
+                                                    uint64_t *__restrict__ out) {
   using F = typename C::Fp;
   constexpr int XW = xyzz_words<F>();
   __shared__ uint32_t park_lds[256 * XW];  // xyzz_add_quad's doubling fallback, per lane
@@ -859,27 +859,15 @@ __global__ void __launch_bounds__(256) k_jobsum_blk(const uint32_t *__restrict__
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) xyzz_store(out + ((size_t)w * c + j) * XW, acc);
-}
-
-// export: XYZZ (device form) -> canonical reference-form coordinates, 4 x NP64 u64
-template <class C>
-__global__ void k_export(const uint32_t *__restrict__ in, int n, uint64_t *__restrict__ out) {
-  using F = typename C::Fp;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n) return;
-  Xyzz<F> p;
-  xyzz_load(p, in + (size_t)g * xyzz_words<F>());
-  uint64_t *o = out + (size_t)g * 4 * F::N64;
-  Fe<F> t;
-  fe_to_ref(t, p.X);
-  fe_store_ref(o + 0 * F::N64, t);
-  fe_to_ref(t, p.Y);
-  fe_store_ref(o + 1 * F::N64, t);
-  fe_to_ref(t, p.ZZ);
-  fe_store_ref(o + 2 * F::N64, t);
-  fe_to_ref(t, p.ZZZ);
-  fe_store_ref(o + 3 * F::N64, t);
+  // export: the 4 lanes of quad 0 hold the sum replicated; lane q writes coordinate q in the
+  // canonical reference form (X, Y, ZZ, ZZZ of NP64 u64 each) for the host
+  if (threadIdx.x < 4) {
+    const int q = (int)threadIdx.x;
+    Fe<F> v, r;
+    fe_sel4(v, acc.X, acc.Y, acc.ZZ, acc.ZZZ, q);
+    fe_to_ref(r, v);
+    fe_store_ref(out + (((size_t)w * c + j) * 4 + q) * C::NP64, r);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -984,7 +972,6 @@ static size_t group_bytes(const MsmShape &s) {
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
   add((size_t)s.W * s.NY * xw);           // Y
-  add((size_t)s.W * s.J * xw);            // per-(window, job) sums
   add((size_t)s.W * s.J * 4 * C::NP64 * 8);  // export
   add(cub > cub2 ? cub : cub2);
   return bytes + (1 << 20);
@@ -1056,7 +1043,7 @@ struct GroupPass {
   bool done = false;
   uint32_t *list, *dig, *tmpv, *cnt, *coff, *offsets, *ikeys0, *ivals0, *ckeys, *cidx, *flags, *pos, *ccount;
   uint16_t *tmpf;
-  uint32_t *okA, *ovA, *okB, *ovB, *buckets, *Y, *P0;
+  uint32_t *okA, *ovA, *okB, *ovB, *buckets, *Y;
   uint64_t *exp;
   void *cubtmp;
   // stitch state (level ping-pong)
@@ -1095,7 +1082,6 @@ struct GroupPass {
     ovB = dev.arena.take<uint32_t>(ns1 * xw);
     buckets = dev.arena.take<uint32_t>(nb * xw);
     Y = dev.arena.take<uint32_t>((size_t)s.W * s.NY * xw);
-    P0 = dev.arena.take<uint32_t>((size_t)s.W * s.J * xw);
     exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
     size_t cub2 = 0;
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, cnt, coff, (int)(s.nmat() + 1), st));
@@ -1180,12 +1166,10 @@ struct GroupPass {
     }
     ZK_CHECK(hipGetLastError());
     mark("ysum");
-    hipLaunchKernelGGL(k_jobsum_blk<C>, dim3((unsigned)(s.W * c)), dim3(256), 0, st, Y, c, s.l0, P0);
+    hipLaunchKernelGGL(k_jobsum_blk<C>, dim3((unsigned)(s.W * c)), dim3(256), 0, st, Y, c, s.l0, exp);
     ZK_CHECK(hipGetLastError());
     mark("jobsum");
     const int ngrp = s.W * s.J;
-    hipLaunchKernelGGL(k_export<C>, dim3(div_up(ngrp, 64)), dim3(64), 0, st, P0, ngrp, exp);
-    ZK_CHECK(hipGetLastError());
     ZK_CHECK(hipMemcpyAsync(h, exp, (size_t)ngrp * 4 * C::NP64 * 8, hipMemcpyDeviceToHost, st));
   }
 

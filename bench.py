@@ -254,7 +254,7 @@ def main():
     if not args.no_ntt:
         result["ntt"] = bench_ntt(zk, args, dist)
     if rank == 0 and world == 1 and not args.no_e2e:
-        result["end_to_end"] = end_to_end(zk, curve, scalars, points, ms_per_step, result.get("ntt"), args)
+        result["end_to_end"] = end_to_end(zk, curve, scalars, points, ms_per_step, result.get("ntt"), args, aff)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(zk, curve, seed, args.cpu_msm_log, args.cpu_ntt_log)
     d_s.free()
@@ -277,6 +277,8 @@ def msm_rooflines(curve, n, c, accum_s):
                         "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
                         "traffic_source": (pmc or {}).get("source"),
                         "kernel": "k_accum (bucket accumulation)", "kernel_ms": accum_s * 1e3,
+                        "kernel_ms_source": "HIP events recorded around every k_accum launch on the library's "
+                                            "own stream (zkg_timer_*), averaged over the timed steps",
                         "algorithmic_bytes_per_launch": algo_bytes,
                         "note": "MSM is VALU-issue bound (integer multiply-add), see valu_roofline"}}
     ceil = valu_ceiling()
@@ -321,6 +323,7 @@ def bench_ntt(zk, args, dist):
            "unit": "elems/s", "n_gpus": dist.world,
            "scaling": "weak (one independent 2^24 transform per GPU)" if dist.world > 1 else "single"}
     ceil = valu_ceiling()
+    isa_src, isa = latest_profile("*isa_k_ntt_pass.json")
     for name, src, dst, inv in (("forward", d_x, d_f, False), ("inverse", d_f, d_i, True)):
         dist.barrier()
         zk.timer(enable=True, reset=True)
@@ -339,16 +342,39 @@ def bench_ntt(zk, args, dist):
         if ceil:
             mads = products * 2 * FR_LIMBS * FR_LIMBS
             r["valu_roofline"] = {"fr_products": products, "v_mad_u64_u32": mads,
-                                  "unit": "v_mad_u64_u32/s", "achieved": mads / kt, "peak": ceil["mad_rate"],
+                                  "unit": "v_mad_u64_u32/s", "mad_only_achieved": mads / kt, "peak": ceil["mad_rate"],
                                   "mad_only_frac": mads / kt / ceil["mad_rate"], "peak_source": ceil["source"]}
+            model = (isa or {}).get("curves", {}).get(curve, {}).get("transforms", {}).get(f"m{m}_{name}")
+            if model:
+                slots = model["issue_slots"]
+                r["valu_roofline"].update({
+                    "bound": "VALU issue", "issue_slots_per_transform": slots, "unit": "half-rate issue slots/s",
+                    "achieved": slots / kt, "frac": slots / kt / ceil["mad_rate"],
+                    "count_source": f"{isa_src}: static issue slots of every k_ntt_pass loop x its trip count "
+                                    "per launch shape, summed over the passes (tools/ntt_isa_model.py)"})
         res[name] = r
     res["value"] = res["forward"]["elems_per_s"]
+    # cold call: the first transform after zkg_release (working-set arena allocated and the
+    # per-(m, generator, direction) twiddle tables built inside the call), beside the warm one
+    zk.load().zkg_device_synchronize()
+    zk.release()
+    dist.barrier()
+    t0 = time.perf_counter()
+    zk.ntt_device(curve, m, g, d_x, d_f)
+    zk.load().zkg_device_synchronize()
+    res["forward"]["cold_ms"] = (time.perf_counter() - t0) * 1e3
+    res["forward"]["cold_note"] = ("first call after zkg_release: arena hipMalloc + twiddle-table build "
+                                   "(k_tw_tables / k_tw_inner / k_tw_pass, 512 MiB pass-0 table) + the transform")
     f = d_f.to_host(x)
     back = d_i.to_host(x)
+    zk.ntt_device(curve, m, g, d_x, d_i, inverse=True)  # the inverse of the config input itself
+    ix = d_i.to_host(x)
     cfg = baseline().get("config3_bls12_381_ntt_2^24")
+    ok = cfg and cfg["log_n"] == m
     res["parity_vs_reference"] = {
-        "forward_sha256_match": (hashlib.sha256(f.tobytes()).hexdigest() == cfg["forward_sha256"])
-        if cfg and cfg["log_n"] == m else None,
+        "forward_sha256_match": (hashlib.sha256(f.tobytes()).hexdigest() == cfg["forward_sha256"]) if ok else None,
+        "inverse_sha256_match": (hashlib.sha256(ix.tobytes()).hexdigest() == cfg.get("inverse_sha256"))
+        if ok and "inverse_sha256" in cfg else None,
         "roundtrip_exact": bool(np.array_equal(back, x)),
     }
     for b in (d_x, d_f, d_i):
@@ -356,7 +382,7 @@ def bench_ntt(zk, args, dist):
     return res
 
 
-def end_to_end(zk, curve, scalars, points, device_ms, ntt, args, reps=5):
+def end_to_end(zk, curve, scalars, points, device_ms, ntt, args, device_aff, reps=5):
     """The reference-named entry points with HOST buffers, as the Haskell binding calls them
     (inputs cross PCIe every call; caller memory is ordinary pageable memory)."""
     import numpy as np
@@ -371,7 +397,7 @@ def end_to_end(zk, curve, scalars, points, device_ms, ntt, args, reps=5):
     out["msm"] = {"symbol": f"{curve}_G1_proj_MSM_mont_coeff_affine_out", "pairs_per_s": n / dt, "ms": dt * 1e3,
                   "device_resident_ms": device_ms, "h2d_bytes": h2d,
                   "h2d_GBps_effective": h2d / max(dt - device_ms * 1e-3, 1e-9) / 1e9,
-                  "matches_device_resident": None}
+                  "matches_device_resident": bool(np.array_equal(aff, device_aff))}
     if ntt and not args.no_ntt:
         m = args.ntt_log
         x = zk.gen_fr("bls12_381", 0x5A4B0003, 1 << m)

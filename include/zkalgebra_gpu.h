@@ -208,6 +208,20 @@ ZKG_API void zkg_memcpy_htod(void *dst, const void *src, size_t bytes);
 ZKG_API void zkg_memcpy_dtoh(void *dst, const void *src, size_t bytes);
 ZKG_API void zkg_device_synchronize(void);
 
+/* Device set of the host-buffer MSM entry points (G1 and G2, every Part-1 MSM symbol): the
+ * pairs are split into n contiguous chunks, chunk k computed on device ids[k] (copying only its
+ * own chunk over that device's PCIe link), the partial sums added in list order.  A device may
+ * be listed more than once (one stream / arena per occurrence).  n <= 1: the calling thread's
+ * device only (the default; also set by the environment variable ZKG_DEVICES = "all" or
+ * "0,1,..." at first use).  Returns 0, or -1 (set unchanged) for an invalid id.  The
+ * device-resident zkg_*_device calls always run on the calling thread's device. */
+ZKG_API int zkg_set_devices(const int *ids, int n);
+ZKG_API int zkg_get_devices(int *ids, int cap);  /* returns the set's size; copies min(size, cap) ids */
+
+/* Frees every device buffer the library holds (per-device working-set arenas, pinned staging,
+ * cached NTT twiddle tables) after waiting for the calls in flight; later calls re-allocate. */
+ZKG_API void zkg_release(void);
+
 /* device-resident MSM: d_expos / d_grps are DEVICE pointers (already in HBM);
  * tgt_proj is a HOST buffer of 3*NP u64 receiving the normalised projective sum. */
 ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,
@@ -247,10 +261,6 @@ ZKG_API void zkg_gen_g1_points(int curve, uint64_t seed, int64_t start, int64_t 
  * (Class/FFT.hs:60-66; BLS12_381/Fr/Mont.hs:145-151, BN128/Fr/Mont.hs:146-148) */
 ZKG_API void zkg_fft_generator(int curve, int m, uint64_t *out);
 
-/* live VALU roofline probe: Montgomery products per second of the device field engine;
- * field: 0 = bn128 Fp, 1 = bn128 Fr, 2 = bls12_381 Fp, 3 = bls12_381 Fr */
-ZKG_API double zkg_field_mul_rate(int field);
-
 /* MSM window heuristic used when window_size is not given */
 ZKG_API int zkg_msm_default_window(int npoints);
 
@@ -262,6 +272,18 @@ ZKG_API void zkg_msm_set_group_limit(size_t entries);
 /* test hook: NTT pass split -- 12: two passes of 2^9..2^12-point DFTs (4096-element tiles) for
  * every 2^17..2^24; 8: passes of <= 2^8-point DFTs only; 0: the default (two passes at 2^20 only) */
 ZKG_API void zkg_ntt_set_max_radix(int r);
+/* test hook: inter-pass twiddle table entries above which an NTT pass computes its twiddles on
+ * the fly (default 2^25, i.e. only transforms of 2^26 and more; 0 restores it) */
+ZKG_API void zkg_ntt_set_table_max(size_t entries);
+/* test hook: device bytes one working-set arena may hold (0: unlimited), to exercise the
+ * out-of-memory degrade path (smaller MSM window groups) */
+ZKG_API void zkg_arena_set_limit(size_t bytes);
+/* window groups (pipeline passes) of the most recent single-device MSM pass */
+ZKG_API int zkg_msm_last_groups(void);
+/* device bytes of one G1 MSM's working set (the arena it reserves) with its windows split into
+ * `groups` passes; window_size <= 0: the default window */
+ZKG_API size_t zkg_msm_workspace_bytes(int curve, int npoints, int expo_nlimbs, int expos_mont, int host_inputs,
+                                       int window_size, int groups);
 
 /* timing probe of the dominant kernel (MSM bucket accumulation / NTT pass chain),
  * measured with HIP events on each device's own stream; read sums over devices */

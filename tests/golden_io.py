@@ -25,3 +25,98 @@ def ntt_cases(curve):
 def baseline_configs():
     p = os.path.join(GOLD, "baseline_configs.json")
     return json.load(open(p)) if os.path.exists(p) else {}
+
+
+# --------------------------------------------------------------------------- adversarial NTT inputs
+# Raw Montgomery words chosen to drive the lazy butterflies and the closing reduction to their
+# extremes (largest canonical limbs, sign flips between neighbours, all-zero columns).  Shared by
+# tools/make_golden.py (reference digests) and the tests.
+FR_ORDER = {
+    "bn128": 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001,
+    "bls12_381": 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001,
+}
+NTT_PATTERNS = ("all_rm1", "alt_0_rm1", "delta_one", "delta_rm1", "constant", "descending")
+
+
+def _words(x):
+    return np.array([(x >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+
+
+def fr_int(row):
+    return sum(int(row[i]) << (64 * i) for i in range(4))
+
+
+def mont_one(curve):
+    return (1 << 256) % FR_ORDER[curve]
+
+
+PATTERN_CONST = 0x1F2E3D4C5B6A79880123456789ABCDEF00112233445566778899AABBCCDDEEFF
+
+
+def ntt_pattern(curve, name, m):
+    """raw Montgomery words of pattern `name` at size 2^m"""
+    r = FR_ORDER[curve]
+    n = 1 << m
+    x = np.zeros((n, 4), dtype=np.uint64)
+    if name == "all_rm1":
+        x[:] = _words(r - 1)
+    elif name == "alt_0_rm1":
+        x[1::2] = _words(r - 1)
+    elif name == "delta_one":
+        x[0] = _words(mont_one(curve))
+    elif name == "delta_rm1":
+        x[0] = _words(r - 1)
+    elif name == "constant":
+        x[:] = _words(PATTERN_CONST % r)
+    elif name == "descending":  # r-1, r-2, ...: the largest distinct canonical words
+        lo = (r - 1) & 0xFFFFFFFFFFFFFFFF
+        assert lo >= n
+        x[:] = _words(r - 1)
+        x[:, 0] = np.uint64(lo) - np.arange(n, dtype=np.uint64)
+    else:
+        raise KeyError(name)
+    return x
+
+
+def ntt_pattern_expected(curve, name, m, inverse):
+    """closed form of the NTT of the constant / delta / alternating patterns (raw Montgomery words
+    are linear: mont(a x) = a mont(x)), or None for patterns without one.  Returns a dict
+    {index: raw value}; every other output is 0."""
+    r = FR_ORDER[curve]
+    n = 1 << m
+    ninv = pow(n, -1, r)
+    rm1 = r - 1
+    if name in ("all_rm1", "constant"):
+        c = rm1 if name == "all_rm1" else PATTERN_CONST % r
+        return {0: c % r} if inverse else {0: n * c % r}
+    if name in ("delta_one", "delta_rm1"):
+        d = mont_one(curve) if name == "delta_one" else rm1
+        v = d * ninv % r if inverse else d
+        return {"all": v}
+    if name == "alt_0_rm1":
+        if m == 0:
+            return {0: 0}
+        # sum over odd j of a w^(+-jk) = a w^(+-k) (n/2) [k in {0, n/2}]; w^(n/2) = -1
+        half = n // 2
+        s = rm1 * (ninv if inverse else 1) % r
+        return {0: s * half % r, half: (r - s * half % r) % r}
+    return None
+
+
+def check_pattern_output(curve, name, m, inverse, out):
+    """True / False against the closed form, None when the pattern has none"""
+    exp = ntt_pattern_expected(curve, name, m, inverse)
+    if exp is None:
+        return None
+    n = 1 << m
+    if "all" in exp:
+        return bool(np.all(out == _words(exp["all"])))
+    want = np.zeros((n, 4), dtype=np.uint64)
+    for k, v in exp.items():
+        want[k] = _words(v)
+    return bool(np.array_equal(out, want))
+
+
+def ntt_patterns_golden():
+    p = os.path.join(GOLD, "ntt_patterns.json")
+    return json.load(open(p)) if os.path.exists(p) else {}

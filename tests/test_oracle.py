@@ -50,3 +50,30 @@ def test_naive_equals_bucket(oracle, zk, curve):
     sc = oracle.to_std(1 if curve == "bn128" else 3, zk.gen_fr(curve, 15, 30))
     pts = zk.gen_points(curve, 16, 30)
     assert np.array_equal(oracle.msm_naive(curve, sc, pts), oracle.msm(curve, sc, pts, mont=False))
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_oracle_ntt_patterns_vs_reference_digests(oracle, zk, curve):
+    """the oracle's NTT / iNTT on the adversarial inputs (golden_io.NTT_PATTERNS) against the
+    reference's own digests (tools/make_golden.py patterns) and the closed forms"""
+    import hashlib
+    from golden_io import NTT_PATTERNS, check_pattern_output, ntt_pattern, ntt_patterns_golden
+    cases = ntt_patterns_golden()["cases"]
+    for m in (5, 12, 14):
+        g = zk.get_fft_subgroup(curve, m).gen_array()
+        for name in NTT_PATTERNS:
+            x = ntt_pattern(curve, name, m)
+            for inverse in (False, True):
+                y = oracle.ntt(curve, m, g, x, inverse=inverse)
+                key = f"{curve}/{name}/m{m}/{'inverse' if inverse else 'forward'}"
+                assert hashlib.sha256(y.tobytes()).hexdigest() == cases[key]["sha256"], key
+                assert check_pattern_output(curve, name, m, inverse, y) in (None, True), key
+
+
+def test_ntt_pattern_closed_forms_are_pinned():
+    """every closed form the GPU tests use at 2^22..2^26 was confirmed by the reference itself
+    at m = 5, 12, 14 and 20 when the fixtures were generated"""
+    from golden_io import ntt_patterns_golden
+    cases = ntt_patterns_golden()["cases"]
+    checked = [k for k, v in cases.items() if v["reference_closed_form_ok"] is not None]
+    assert len(checked) == 80 and all(cases[k]["reference_closed_form_ok"] for k in checked)

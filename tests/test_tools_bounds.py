@@ -14,10 +14,38 @@ def _load(name):
     return spec, mod
 
 
-def test_lazy_madd_bounds_bn254():
+def test_lazy_bounds_all_paths():
+    """every lazy path (both MSM base fields' mixed and full additions, the NTT butterflies of
+    every radix, the closing reductions, the scalar REDC) satisfies its limb / value bounds"""
     spec, mod = _load("lazy_bounds")
     spec.loader.exec_module(mod)
-    assert mod.check_bn254()
+    ok, results = mod.run_all(verbose=False)
+    assert ok, [r for r in results if r[2] != "ok"]
+    assert len(results) == 10
+
+
+def test_lazy_bounds_catch_a_broken_invariant():
+    """the checker is not vacuous: the once-documented 381-bit Y < 6p form, a twiddle bounded
+    only by 2p after 2^12-point DFTs, and a too-small K in a lazy difference are rejected"""
+    spec, mod = _load("lazy_bounds")
+    spec.loader.exec_module(mod)
+    F = mod.Field("bls12_381_fp")
+    y6 = F.norm_val(6 * F.p)
+    try:
+        F.sub_lazy(F.zero(), y6, 6, 1)
+        raise AssertionError("Y < 6p accepted")
+    except mod.BoundError:
+        pass
+    Fr = mod.Field("bls12_381_fr")
+    out = mod.ntt_lds_dft(Fr, 12, Fr.norm_val(Fr.p))
+    w = Fr.norm_val(2 * Fr.p)  # a twiddle only known to be < 2p (tw2's product is < 1.02p)
+    y = Fr.mul(out, w)
+    assert y.val > 2 * Fr.p  # 2^12-point DFT outputs (< 50p) times 2p exceed p R' (R'/p = 70.7)
+    try:
+        F.sub_lazy(F.norm_val(2 * F.p), F.norm_val(14 * F.p), 8, 1)
+        raise AssertionError("b < 14p accepted under K = 8")
+    except mod.BoundError:
+        pass
 
 
 def test_ntt_swizzle_conflict_free():

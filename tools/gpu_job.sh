@@ -26,7 +26,7 @@ BENCH_SHORT="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --ntt-step
 for step in "$@"; do
   echo "[$(date +%T)] step $step"
   case $step in
-    tests) timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > ${O}_tests.log 2>&1 ;;
+    tests) timeout -k 10 ${TESTS_TIMEOUT:-900} python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > ${O}_tests.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 ;;
     bench) timeout -k 10 400 python -u bench.py > ${O}_bench.json 2> ${O}_bench.err ;;
     bench2) timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

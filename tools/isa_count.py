@@ -30,7 +30,8 @@ def function_body(lines, sym):
 
 def blocks_of(body):
     blocks = []
-    cur = {"label": "entry", "loop": None, "depth": 0, "ops": collections.Counter(), "n": 0}
+    cur = {"label": "entry", "loop": None, "depth": 0, "ops": collections.Counter(), "n": 0, "succ": [],
+           "falls": True}
     for l in body[1:]:
         m = re.match(r"^(\.LBB\w+):(.*)$", l)
         if m:
@@ -44,7 +45,8 @@ def blocks_of(body):
                 loop, depth = hm.group(1), int(hm.group(2))
             else:
                 loop, depth = None, 0
-            cur = {"label": m.group(1), "loop": loop, "depth": depth, "ops": collections.Counter(), "n": 0}
+            cur = {"label": m.group(1), "loop": loop, "depth": depth, "ops": collections.Counter(), "n": 0,
+                   "succ": [], "falls": True}
             continue
         s = l.strip()
         if not s or s.startswith(";") or s.startswith(".") or s.endswith(":"):
@@ -52,8 +54,62 @@ def blocks_of(body):
         op = s.split()[0]
         cur["ops"][op] += 1
         cur["n"] += 1
+        if op.startswith("s_branch") or op.startswith("s_cbranch") or op.startswith("s_setpc"):
+            t = re.search(r"(\.LBB\w+)", s)
+            if t:
+                cur["succ"].append(t.group(1))
+            if op.startswith("s_branch") or op.startswith("s_setpc"):
+                cur["falls"] = False
+        if op.startswith("s_endpgm"):
+            cur["falls"] = False
     blocks.append(cur)
     return blocks
+
+
+def cfg_loops(blocks):
+    """natural loops from the control-flow graph (branch targets + fall-through): an edge i -> h
+    whose target dominates its source is a back edge; the loop is the header plus every block
+    that reaches the back edge's source without passing through the header.  (LLVM's "in Loop"
+    comments miss blocks whose label carries another comment.)"""
+    idx = {b["label"]: i for i, b in enumerate(blocks)}
+    succ = []
+    for i, b in enumerate(blocks):
+        s = [idx[t] for t in b["succ"] if t in idx]
+        if b["falls"] and i + 1 < len(blocks):
+            s.append(i + 1)
+        succ.append(s)
+    pred = [[] for _ in blocks]
+    for i, ss in enumerate(succ):
+        for j in ss:
+            pred[j].append(i)
+    # dominators (iterative data flow from the entry block)
+    n = len(blocks)
+    full = set(range(n))
+    dom = [full.copy() for _ in range(n)]
+    dom[0] = {0}
+    changed = True
+    while changed:
+        changed = False
+        for i in range(1, n):
+            ps = [dom[p] for p in pred[i]]
+            new = (set.intersection(*ps) if ps else set()) | {i}
+            if new != dom[i]:
+                dom[i] = new
+                changed = True
+    loops = collections.OrderedDict()
+    for i, ss in enumerate(succ):
+        for h in ss:
+            if h in dom[i]:  # back edge i -> h (h dominates i)
+                body = loops.setdefault(blocks[h]["label"], {h})
+                stack = [i]
+                while stack:
+                    x = stack.pop()
+                    if x in body:
+                        continue
+                    body.add(x)
+                    stack.extend(pred[x])
+    # keep innermost-first order by header position
+    return collections.OrderedDict((k, sorted(v)) for k, v in sorted(loops.items(), key=lambda kv: idx[kv[0]]))
 
 
 def classify(op):
@@ -88,11 +144,26 @@ def main():
     for b in blocks:
         total.update(b["ops"])
     print(f"{name}: {sum(total.values())} instructions, {total['v_mad_u64_u32']} v_mad_u64_u32 (static)")
+    # loops as LLVM annotates them ("in Loop: Header=..." on the block labels): for k_accum these
+    # are exactly the blocks of one mixed add (its rare branches -- doubling, flush, infinity --
+    # carry other comments), which is what the VALU roofline prices
     loops = collections.OrderedDict()
     for b in blocks:
         if b["loop"]:
             loops.setdefault(b["loop"], []).append(b)
-    out = {"function": name, "note": a.note, "static_total": dict(total), "blocks": [], "loops": {}}
+    # natural loops of the control-flow graph: every block of each loop (tools/ntt_isa_model.py)
+    out_cfg = collections.OrderedDict()
+    for hdr, members in cfg_loops(blocks).items():
+        cls = collections.Counter()
+        for i in members:
+            for op, c in blocks[i]["ops"].items():
+                cls[classify(op)] += c
+        out_cfg[hdr[2:] if hdr.startswith(".L") else hdr] = {
+            "blocks": [blocks[i]["label"] for i in members], "classes": dict(cls),
+            "issue_slots": cls.get("v_mad_u64_u32", 0) + cls.get("v_mul32", 0) + cls.get("valu_64", 0) +
+            0.5 * cls.get("valu_other", 0)}
+    out = {"function": name, "note": a.note, "static_total": dict(total), "blocks": [], "loops": {},
+           "cfg_loops": out_cfg}
     print(f"{'block':<14}{'loop':<12}{'d':>2}{'instr':>7}{'mad64':>7}{'valu':>7}{'vmem':>6}{'lds':>6}")
     for b in blocks:
         cls = collections.Counter()
@@ -103,6 +174,9 @@ def main():
               f"{cls['v_mad_u64_u32'] + cls['v_mul32'] + cls['valu_64'] + cls['valu_other']:>7}{cls['vmem']:>6}{cls['lds']:>6}")
         out["blocks"].append({"label": b["label"], "loop": b["loop"], "depth": b["depth"], "instr": b["n"],
                               "classes": dict(cls)})
+    for hdr, d in out_cfg.items():
+        print(f"cfg loop {hdr}: {len(d['blocks'])} blocks, {d['issue_slots']:.1f} issue slots, "
+              + ", ".join(f"{k}={v}" for k, v in sorted(d["classes"].items())))
     for lp, bl in loops.items():
         cls = collections.Counter()
         for b in bl:

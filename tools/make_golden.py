@@ -8,8 +8,11 @@ reference's own generated C (oracle/_ref/libzkref.so, built in place from
 the documented synthetic-input generator (zikkurat-algebra_amd/csrc/zk_gen.cpp; an
 independent restatement in oracle/zk_oracle.c is checked equal by the tests).
 
-  python tools/make_golden.py small   # edge-case MSM + NTT vectors (stored in full)  ~1 min
-  python tools/make_golden.py large   # BASELINE-config outputs / SHA-256 digests     ~10 min, 8 cores
+  python tools/make_golden.py small     # edge-case MSM + NTT vectors (stored in full)  ~1 min
+  python tools/make_golden.py large     # BASELINE-config outputs / SHA-256 digests     ~10 min, 8 cores
+  python tools/make_golden.py patterns  # adversarial NTT inputs (tests/golden_io.py NTT_PATTERNS) at
+                                        # m = 5, 12, 14, 20 and random 2^20 vectors: reference forward /
+                                        # inverse SHA-256 digests -> tests/golden/ntt_patterns.json   ~1 min
 
 Only this script (in this container, where /root/reference exists) runs the reference;
 the GPU box only reads the committed .npz/.json files.
@@ -29,6 +32,8 @@ sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
 GOLD = os.path.join(ROOT, "tests", "golden")
 
 from oracle.oracle import Reference, Oracle  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import golden_io  # noqa: E402  (pattern definitions shared with the tests)
 import zkalgebra as zk  # noqa: E402  (host-only functions: generator, fft generator)
 
 R_ORDER = {
@@ -163,6 +168,41 @@ def large_msm(curve, logn, seed, shards):
             "reference_entry": "MSM_mont_coeff_proj_out" if mont else "MSM_std_coeff_proj_out (to_std scalars)"}
 
 
+# ----------------------------------------------------------------------------- adversarial NTT patterns
+
+PATTERN_SIZES = (5, 12, 14, 20)
+RANDOM_SEED = 0x5A4B0003
+
+
+def _pattern_job(args):
+    curve, name, m, inverse = args
+    ref = Reference()
+    g = zk.get_fft_subgroup(curve, m).gen_array()
+    x = zk.gen_fr(curve, RANDOM_SEED, 1 << m) if name == "random" else golden_io.ntt_pattern(curve, name, m)
+    t = time.time()
+    y = ref.ntt(curve, m, g, x, inverse=inverse)
+    dt = time.time() - t
+    closed = None if name == "random" else golden_io.check_pattern_output(curve, name, m, inverse, y)
+    return (f"{curve}/{name}/m{m}/{'inverse' if inverse else 'forward'}",
+            {"sha256": sha(y), "input_sha256": sha(x), "first": [int(v) for v in y[0]],
+             "reference_closed_form_ok": closed, "reference_seconds": dt})
+
+
+def make_patterns():
+    jobs = [(c, nm, m, inv) for c in zk.CURVES for nm in golden_io.NTT_PATTERNS for m in PATTERN_SIZES
+            for inv in (False, True)]
+    jobs += [(c, "random", 20, inv) for c in zk.CURVES for inv in (False, True)]
+    with mp.Pool(8) as pool:
+        res = dict(pool.map(_pattern_job, jobs))
+    bad = [k for k, v in res.items() if v["reference_closed_form_ok"] is False]
+    assert not bad, f"the reference disagrees with the closed forms: {bad}"
+    out = {"generator": "tools/make_golden.py patterns (reference lib/cbits, oracle/_ref)",
+           "random_seed": RANDOM_SEED, "cases": res}
+    json.dump(out, open(os.path.join(GOLD, "ntt_patterns.json"), "w"), indent=1, sort_keys=True)
+    print(len(res), "pattern digests;", sum(1 for v in res.values() if v["reference_closed_form_ok"]),
+          "also match the closed forms")
+
+
 def large_ntt(curve, logn, seed):
     ref = Reference()
     g = zk.get_fft_subgroup(curve, logn).gen_array()
@@ -174,8 +214,11 @@ def large_ntt(curve, logn, seed):
     i = ref.ntt(curve, logn, g, f, inverse=True)
     ti = time.time() - t
     assert np.array_equal(i, x), "reference NTT round trip failed"
+    t = time.time()
+    ix = ref.ntt(curve, logn, g, x, inverse=True)  # the inverse applied to the config input itself
     return {"curve": curve, "log_n": logn, "seed": seed, "input_sha256": sha(x), "forward_sha256": sha(f),
             "forward_first": [int(v) for v in f[0]], "forward_last": [int(v) for v in f[-1]],
+            "inverse_sha256": sha(ix), "inverse_first": [int(v) for v in ix[0]],
             "roundtrip_ok": True, "reference_forward_seconds": tf, "reference_inverse_seconds": ti}
 
 
@@ -201,10 +244,12 @@ def make_large(which):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) < 2 or sys.argv[1] not in ("small", "large"):
+    if len(sys.argv) < 2 or sys.argv[1] not in ("small", "large", "patterns"):
         print(__doc__)
         sys.exit(2)
     if sys.argv[1] == "small":
         make_small()
+    elif sys.argv[1] == "patterns":
+        make_patterns()
     else:
         make_large(sys.argv[2] if len(sys.argv) > 2 else None)

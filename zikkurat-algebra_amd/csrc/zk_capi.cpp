@@ -15,7 +15,6 @@
 #include "zk_ntt.hpp"
 #include "zk_runtime.hpp"
 
-namespace zk { double field_mul_rate(int field); }  // zk_probe.hip
 using namespace zk;
 
 namespace {
@@ -277,7 +276,35 @@ ZKG_API void zkg_msm_profile(int on) { zk::msm_set_profile(on); }
 ZKG_API void zkg_msm_set_group_limit(size_t entries) { zk::msm_set_group_limit(entries); }
 ZKG_API void zkg_ntt_set_max_radix(int r) { zk::ntt_set_max_radix(r); }
 
-ZKG_API double zkg_field_mul_rate(int field) { return zk::field_mul_rate(field); }
+ZKG_API void zkg_ntt_set_table_max(size_t entries) { zk::ntt_set_table_max(entries); }
+ZKG_API void zkg_arena_set_limit(size_t bytes) { zk::arena_set_limit(bytes); }
+ZKG_API int zkg_msm_last_groups(void) { return zk::msm_last_groups_read(); }
+ZKG_API size_t zkg_msm_workspace_bytes(int curve, int npoints, int expo_nlimbs, int expos_mont, int host_inputs,
+                                       int window_size, int groups) {
+  if (curve == ZKG_BN128)
+    return zk::msm_workspace_bytes<BN254>(npoints, expo_nlimbs, expos_mont != 0, host_inputs != 0, window_size, groups);
+  return zk::msm_workspace_bytes<BLS381>(npoints, expo_nlimbs, expos_mont != 0, host_inputs != 0, window_size, groups);
+}
+
+ZKG_API int zkg_set_devices(const int *ids, int n) { return zk::set_device_set(ids, n); }
+ZKG_API int zkg_get_devices(int *ids, int cap) {
+  const std::vector<int> v = zk::device_set();
+  for (int i = 0; i < (int)v.size() && i < cap; i++) ids[i] = v[i];
+  return (int)v.size();
+}
+
+ZKG_API void zkg_release(void) {
+  int prev = 0;
+  ZK_CHECK(hipGetDevice(&prev));
+  for (Device *d : all_devices()) {
+    std::lock_guard<std::mutex> lock(d->mu);
+    ZK_CHECK(hipSetDevice(d->id));
+    ZK_CHECK(hipStreamSynchronize(d->stream));
+    zk::ntt_release(*d);
+    d->release_memory();
+  }
+  ZK_CHECK(hipSetDevice(prev));
+}
 
 ZKG_API void zkg_timer_enable(int on) { timer_set_enabled(on != 0); }
 ZKG_API void zkg_timer_reset(void) { timer_reset_all(); }

@@ -150,13 +150,15 @@ __device__ __forceinline__ void xyzz_add_aff(Xyzz<F> &acc, const Aff<F> &a) {
 // squares PP and RR (products are < 2p and normalised, and PP == 0 <=> P == 0 as p is
 // prime), and Y3 = R (Q - X3) - Y1 PPP is one fe_mul2 (shared reduction).
 // Representation invariant of acc between calls: X, Y normalised limbs with values
-// X < 14p, Y < 6p (not < 2p); ZZ, ZZZ < 2p.  The accumulator is stored in this form:
-// every later consumer takes X and Y only into products (which accept it).  Bounds (BLS12-381 Fp: 14 x 28-bit limbs, R'/p > 2^11):
+// X < 14p, Y < 2p; ZZ, ZZZ < 2p.  The accumulator is stored in this form: every later
+// consumer takes X only into products (which accept it).  Bounds (BLS12-381 Fp: 14 x 28-bit
+// limbs, R'/p > 2^11), all checked mechanically by tools/lazy_bounds.py (tests/test_tools_bounds.py):
 //   P = U2 + 16p - X1 < 18p, limbs < 2^29.6;  R = S2 + 8p - Y1 < 10p
 //   PP, RR, PPP, Q < 2p (products of values < 2^11 p)
 //   X3 = RR + 4p - PPP + 8p - 2Q < 14p;  t = Q + 16p - X3 < 18p
-//   Y3 = (R t + (6p - Y1) PPP) / R' < 2p... then + 0: Y3 < 2p < 6p
-// Column sums in fe_mul2 (R t: limbs < 2^29.6 each; (6p - Y1): < 2^29.6) stay < 2^64.
+//   Y3 = (R t + (6p - Y1) PPP) / R' < 1.06p
+// Column sums in fe_mul2 (R t: limbs < 2^29.6 each; (6p - Y1): < 2^29.6) stay < 2^64.  (The
+// once-documented Y < 6p would break 6p - Y1's top-limb borrow; every producer gives Y < 1.06p.)
 template <class F>
 __device__ __forceinline__ void xyzz_add_aff_lazy(Xyzz<F> &acc, const Aff<F> &a) {
   static_assert(F::N == 14 && F::RB == 28, "lazy madd bounds are derived for the 14 x 28-bit field");
@@ -182,7 +184,7 @@ __device__ __forceinline__ void xyzz_add_aff_lazy(Xyzz<F> &acc, const Aff<F> &a)
   fe_norm(X3);
   fe_sub_lazy<F, 16, 1>(t, Q, X3);        // Q - X3
   Fe<F> ny;
-  fe_sub_lazy<F, 6, 1>(ny, Fe<F>{}, acc.Y);  // 6p - Y1 (acc.Y < 6p, normalised)
+  fe_sub_lazy<F, 6, 1>(ny, Fe<F>{}, acc.Y);  // 6p - Y1 (acc.Y < 2p, normalised)
   fe_mul2(acc.Y, R, t, ny, PPP);          // Y3 = R (Q - X3) - Y1 PPP
   acc.X = X3;
   fe_mul(acc.ZZ, acc.ZZ, PP);
@@ -280,7 +282,7 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
 
 // acc += b (add-2008-s) for the G1 reductions (Y sums), with lazy differences and the shared-
 // reduction Y3 of the lazy mixed adds above.  Inputs in the bucket forms (381-bit: X < 14p,
-// Y < 6p; 254-bit: X, Y < 2p), output in the same form (Y3 < 2p).  Bounds, in units of p:
+// Y < 2p; 254-bit: X, Y < 2p), output in the same form.  Bounds (tools/lazy_bounds.py), in units of p:
 //   381-bit: P = U2 + 4p - U1 < 6p, R = S2 + 4p - S1 < 6p, X3 < 14p as in the madd,
 //            Y3: R (Q + 16p - X3) + (4p - S1) PPP < (6 * 18 + 4 * 2) p^2 < p R' (R'/p > 2^11)
 //   254-bit: as xyzz_add_aff_lazy9 with U1, S1 (< 2p) in place of X1, Y1

@@ -22,10 +22,13 @@ int msm_default_window(int n) {
 }
 
 void msm_set_profile(int on) { msm_profile_flag().store(on); }
+int msm_last_groups_read() { return msm_last_groups().load(); }
 void msm_set_group_limit(size_t entries) {
   msm_group_limit().store(entries == 0 || entries > MSM_MAX_GROUP_ENTRIES ? MSM_MAX_GROUP_ENTRIES : entries);
 }
 
+template size_t msm_workspace_bytes<BN254>(int, int, bool, bool, int, int);
+template size_t msm_workspace_bytes<BLS381>(int, int, bool, bool, int, int);
 template void msm_g1<BN254>(int, const uint64_t *, int, const uint64_t *, bool, bool, int, uint64_t *);
 template void msm_g1<BLS381>(int, const uint64_t *, int, const uint64_t *, bool, bool, int, uint64_t *);
 

@@ -31,11 +31,15 @@ template <> struct HostOf<BLS381_G2> {
 int msm_default_window(int n);
 void msm_set_profile(int on);  // per-phase event timing of every MSM call, printed to stderr
 void msm_set_group_limit(size_t entries);  // test hook: max sorted entries per pipeline pass (0: default)
+int msm_last_groups_read();  // window groups of the most recent msm_run (degrade-path tests)
 
 // scalars: n x nl u64 (Montgomery Fr if mont, else plain integers of 64 nl bits, any nl >= 1)
 // points : n x 2*NP64 u64 affine Montgomery (all-0xFF = infinity)
 // out    : 3*NP64 u64 projective, reference Montgomery form, NOT normalised
 // host_inputs: pointers are host memory (staged by the call) vs device-resident
+// device bytes of one pass's working set, windows split into `groups` passes
+template <class C>
+size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int window, int groups);
 template <class C>
 void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs, bool mont,
             int window, uint64_t *out_proj);

@@ -39,6 +39,7 @@
 #include "zk_host.hpp"
 #include "zk_runtime.hpp"
 #include "zk_msm.hpp"
+#include "zk_ntt.hpp"
 
 namespace zk {
 
@@ -378,7 +379,7 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
     uint32_t bbeg = offsets[b], bend = offsets[b + 1];
     uint32_t bnext = offsets[min(b + 2, nb)];  // end of the next bucket, loaded ahead
     bool first_run = true;
-    // Flushes store the accumulator LAZILY (X < 14p, Y < 6p for the 381-bit madd): every
+    // Flushes store the accumulator LAZILY (X < 14p for the 381-bit madd): every
     // consumer (xyzz_add / xyzz_dbl / the job sums' export) takes X and Y only into products, which
     // accept those values.  A settle here would cost two products per flush, paid by the
     // whole wavefront whenever any lane flushes (runs average 32 entries at 2^20).
@@ -435,6 +436,9 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
     head_end = k0 != nb && !(first_run && rpart);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last gather and the head flush have landed
   }
+  // the head flushes (plain stores of the other lanes of this wavefront) are published before
+  // the merge below reads them: release here, acquire before the reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   // Merge across the chunk boundary inside the wavefront: lane t's right-partial last run
   // and lane t+1's head run (flushed to slot 2t+2 during its loop) are the same bucket's run
   // exactly when the run crosses that boundary and ends in chunk t+1 -- one add completes
@@ -444,6 +448,7 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
   const uint32_t nhead = (uint32_t)__shfl_down((int)(head_end ? k0 : nb), 1, 64);
   const bool merge = tail_b != nb && lane < 63 && nhead == tail_b;
   if (__any(merge)) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (merge) {
       const uint32_t *src = ivals + (size_t)(2 * t + 2) * xyzz_words<F>();
       uint32_t wds[xyzz_words<F>()];
@@ -942,8 +947,13 @@ constexpr int stitch_bs() { return xyzz_words<F>() > 64 ? 128 : 256; }
 static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.n + s.CH - 1) / s.CH); }
 static size_t stitch_slots1(const MsmShape &s, int bs) { return 2 * ((stitch_slots0(s) + bs - 1) / bs) + 2; }
 
-// sorted entries of one pipeline pass: hipCUB takes int counts, offsets are u32
+// sorted entries of one pipeline pass: passes of several windows are kept at <= 2^30 entries
+// (memory per pass, swept sizes); a single window of n points is always one pass, so a pass
+// holds at most n < 2^31 entries (the C ABI's int) -- every entry index, offset and point
+// index (with the sign in bit 31) fits a u32, and hipCUB only scans the count matrix and
+// the item flags (far below 2^31 entries)
 constexpr size_t MSM_MAX_GROUP_ENTRIES = (size_t)1 << 30;
+constexpr size_t MSM_MAX_PASS_ENTRIES = ((size_t)1 << 31) - 1;
 // test hook (zkg_msm_set_group_limit): a smaller cap, so tests reach the multi-group path
 // at small sizes; 0 restores the default
 inline std::atomic<size_t> &msm_group_limit() {
@@ -975,6 +985,12 @@ static size_t group_bytes(const MsmShape &s) {
   add((size_t)s.W * s.J * 4 * C::NP64 * 8);  // export
   add(cub > cub2 ? cub : cub2);
   return bytes + (1 << 20);
+}
+
+// window groups (pipeline passes) of the most recent msm_run, for tests of the degrade path
+inline std::atomic<int> &msm_last_groups() {
+  static std::atomic<int> v{0};
+  return v;
 }
 
 // Opt-in phase profile (zkg_msm_profile(1)): HIP events between the phases of every call,
@@ -1059,7 +1075,7 @@ struct GroupPass {
     nb = (size_t)s.W * s.B;
     xw = xyzz_words<F>();
     maxent = (size_t)s.W * n;
-    ZK_REQUIRE(maxent <= MSM_MAX_GROUP_ENTRIES, "msm: window group exceeds the sort capacity (internal sizing bug)");
+    ZK_REQUIRE(maxent <= MSM_MAX_PASS_ENTRIES, "msm: window group exceeds the sort capacity (internal sizing bug)");
     list = dev.arena.take<uint32_t>(maxent);  // bucket-ordered (point index | sign)
     dig = dev.arena.take<uint32_t>(maxent);   // |digit| | sign per (window, point)
     tmpv = dev.arena.take<uint32_t>(maxent);  // level-1 order: values
@@ -1271,16 +1287,31 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   // Signed digits need floor(bits/c) + 1 windows: the top window then holds at most c-1
   // bits plus the carry, i.e. a digit <= 2^(c-1) = B, so no carry leaves it.
   const int W = bits / c + 1;
-  // window groups: one pipeline pass sorts at most MSM_MAX_GROUP_ENTRIES (W n >= 2^31 would
-  // overflow the sort's int count); n < 2^31 (int), so one window always fits
-  const int Wg = (int)std::min<size_t>((size_t)W, std::max<size_t>(1, msm_group_limit().load() / (size_t)n));
-  const MsmShape s = make_shape(n, c, Wg);
+  // window groups: one pipeline pass sorts at most msm_group_limit() entries (2^30 by default)
+  // or one window (n < 2^31 entries, MSM_MAX_PASS_ENTRIES)
+  int Wg = (int)std::min<size_t>((size_t)W, std::max<size_t>(1, msm_group_limit().load() / (size_t)n));
   hipStream_t st = dev.stream;
 
   const size_t sc_bytes = host_inputs ? (size_t)n * sc_in.stride * 8 : 0;
   const size_t pt_bytes = host_inputs ? (size_t)n * 2 * C::NP64 * 8 : 0;
   const size_t int_bytes = (size_t)n * aff_words<F>() * 4;
-  dev.arena.reserve(sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(s));
+  // Working set: when the device cannot hold it, drop this context's cached NTT twiddles, then
+  // halve the windows per pass (the result does not depend on the grouping) down to one window
+  // before giving up -- instead of aborting the caller's process on the first failed hipMalloc.
+  bool dropped_twiddles = false;
+  MsmShape s = make_shape(n, c, Wg);
+  while (!dev.arena.try_reserve(sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(s))) {
+    if (!dropped_twiddles) {
+      ZK_CHECK(hipStreamSynchronize(st));
+      ntt_release(dev);
+      dropped_twiddles = true;
+      continue;
+    }
+    ZK_REQUIRE(Wg > 1, "msm: out of device memory (one window per pass does not fit)");
+    Wg = (Wg + 1) / 2;
+    s = make_shape(n, c, Wg);
+  }
+  msm_last_groups().store((W + Wg - 1) / Wg);
   dev.arena.reset();
   ScalarSlice sc = sc_in;
   const uint64_t *d_pt = points;
@@ -1324,14 +1355,28 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
 // ---------------------------------------------------------------------------
 // public (C++) entry point used by the C ABI layer
 
+// Device bytes of one msm_run's working set (what its arena reserves) with the W windows in
+// `groups` passes -- exposed for memory planning and the degrade-path tests.
 template <class C>
-void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs, bool mont,
-            int window, uint64_t *out_proj) {
+size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int window, int groups) {
+  using F = typename C::Fp;
+  if (n <= 0) return 0;
+  const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
+  const int nread = nl < 4 ? nl : 4;
+  const int W = (mont ? HostOf<C>::Fr::BITS : 64 * nread) / c + 1;
+  const int g = groups < 1 ? 1 : (groups > W ? W : groups);
+  const int Wg = (W + g - 1) / g;
+  const size_t sc_bytes = host_inputs ? (size_t)n * nl * 8 : 0;
+  const size_t pt_bytes = host_inputs ? (size_t)n * 2 * C::NP64 * 8 : 0;
+  const size_t int_bytes = (size_t)n * aff_words<F>() * 4;
+  return sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(make_shape(n, c, Wg));
+}
+
+// One complete MSM on one device context (caller holds dev.mu): every scalar slice.
+template <class C>
+static void msm_xyzz(Device &dev, int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs,
+                     bool mont, int window, zkh::Xyzz<typename HostOf<C>::Fp> &acc) {
   using HF = typename HostOf<C>::Fp;
-  ZK_REQUIRE(nl >= 1, "msm: expo_nlimbs must be >= 1");
-  Device &dev = current_device();
-  std::lock_guard<std::mutex> lock(dev.mu);
-  zkh::Xyzz<HF> acc;
   if (mont || nl <= 4) {
     // Montgomery coefficients: the reference converts the first 4 limbs of each row
     // (Fr_mont_to_std reads 4 limbs, G1_proj.c:637-641); for expo_nlimbs != 4 its result
@@ -1351,6 +1396,45 @@ void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool
       msm_run<C>(dev, n, ScalarSlice{scalars, nl, 4 * j, nread, false}, points, host_inputs, window, r);
       zkh::xyzz_add(acc, acc, r);
     }
+  }
+}
+
+template <class C>
+void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool host_inputs, bool mont,
+            int window, uint64_t *out_proj) {
+  using HF = typename HostOf<C>::Fp;
+  ZK_REQUIRE(nl >= 1, "msm: expo_nlimbs must be >= 1");
+  zkh::Xyzz<HF> acc;
+  const std::vector<int> set = host_inputs ? device_set() : std::vector<int>();
+  const int G = (int)set.size();
+  if (G > 1 && n > 0) {
+    // Host buffers with a device set (zkg_set_devices / ZKG_DEVICES): contiguous chunks
+    // [n k / G, n (k+1) / G), one host thread per listed device (one context per occurrence of
+    // a device id), each copying and computing only its chunk over its own PCIe link; the
+    // partial sums are added in list order.  The affine result equals the unsharded one (a
+    // group sum), and the reference's own call is a single chunk (G1_proj.c:630-644).
+    std::vector<zkh::Xyzz<HF>> part(G);
+    std::vector<std::thread> th;
+    for (int k = 0; k < G; k++) {
+      const size_t lo = (size_t)n * k / G, hi = (size_t)n * (k + 1) / G;
+      int slot = 0;
+      for (int j = 0; j < k; j++) slot += set[j] == set[k];
+      zkh::xyzz_set_inf(part[k]);
+      if (hi == lo) continue;
+      th.emplace_back([&, k, lo, hi, slot] {
+        ZK_CHECK(hipSetDevice(set[k]));
+        Device &d = device_context(set[k], slot);
+        std::lock_guard<std::mutex> lock(d.mu);
+        msm_xyzz<C>(d, (int)(hi - lo), scalars + lo * nl, nl, points + lo * 2 * C::NP64, true, mont, window, part[k]);
+      });
+    }
+    for (auto &t : th) t.join();
+    zkh::xyzz_set_inf(acc);
+    for (int k = 0; k < G; k++) zkh::xyzz_add(acc, acc, part[k]);
+  } else {
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lock(dev.mu);
+    msm_xyzz<C>(dev, n, scalars, nl, points, host_inputs, mont, window, acc);
   }
   zkh::Proj<HF> p;
   zkh::xyzz_to_proj(p, acc);

@@ -162,6 +162,9 @@ __device__ __forceinline__ void lds_put(uint32_t *p, const Fe<F> &x) {
 // input range (R'/p > 68) and fe_reduce_small's (< 64p): the products of the next stage and
 // the pass's closing product (twiddle / scale) or reduction bring them back below 2p.  (The
 // 4096-point tiles add 12 stages: < 50p.)  Limb bound: normalised (< 2^29) at round entry, < 2^31.4 at round exit.
+// Every radix 2^1..2^12, both Fr fields, every closing step (table twiddle, on-the-fly twiddle
+// = a product of two canonical entries < 1.02p, 1/N scale, fe_reduce_small) and the inter-pass
+// fixed point (values < 1.72p between passes) are checked by tools/lazy_bounds.py.
 template <class F, int NT>
 __device__ __forceinline__ void lds_dft(uint32_t *data, const uint32_t *__restrict__ itw, int r, int G) {
   constexpr int NW = F::N;
@@ -281,6 +284,12 @@ struct PassArgs {
 #ifndef ZK_NTT_TABLE_MAX
 #define ZK_NTT_TABLE_MAX ((size_t)1 << 25)
 #endif
+static std::atomic<size_t> g_ntt_table_max{0};  // test hook (ntt_set_table_max); 0 = the default
+void ntt_set_table_max(size_t entries) { g_ntt_table_max.store(entries); }
+static size_t ntt_table_max() {
+  const size_t v = g_ntt_table_max.load();
+  return v ? v : ZK_NTT_TABLE_MAX;
+}
 
 // One pass.  Block = one tile of G instances x R elements.
 //   non-last pass: instance (hi, lo), lo in [0, S); element k at hi*R*S + k*S + lo
@@ -355,43 +364,56 @@ __global__ void __launch_bounds__(NT) k_ntt_pass(const uint64_t *__restrict__ sr
 
   lds_dft<F, NT>(data, itw, r, G);
 
-  Fe<F> sc;
-  if (scale) {
-    Fe<F> t;
+  // Output: one loop per closing mode (uniform per launch), so every mode is its own loop in
+  // the ISA (tools/ntt_isa_model.py prices each pass from these loops)
+  //   non-last pass: x * w, w from the pass's table or (otf) tw2; stored packed, not canonical
+  //                  (a product is < 2p < 2^256; the next pass only multiplies and adds it)
+  //   last pass:     the lazily grown value (< 50p) back below 2p, as fe_store_ref's
+  //                  canonicalisation needs -- by the product with the scale (1/N) when an
+  //                  inverse's scale has no table to ride on, else by a product-free reduction
+  auto out_addr = [&](int g, int k) -> size_t {
+    if (!a.last) return hi_base + (size_t)k * S + g;
+    return (a.P == 1) ? (size_t)k : nat_base + (size_t)(k0base + g) + (size_t)k * a.T;
+  };
+  if (!a.last && !a.otf) {
+    for (int e = tid; e < nel; e += NT) {
+      const int g = e % G, k = e / G;  // consecutive threads -> consecutive g (coalesced)
+      Fe<F> x, w, y;
+      lds_get(x, data + (size_t)lds_slot((uint32_t)(g * R + k)) * NW);
+      const size_t addr = out_addr(g, k);
+      fe_load_ref(w, tab + ((size_t)k * S + (addr % S)) * F::N64);
+      fe_mul(y, x, w);
+      fe_store_packed(dst + addr * F::N64, y);
+    }
+  } else if (!a.last) {
+    for (int e = tid; e < nel; e += NT) {
+      const int g = e % G, k = e / G;
+      Fe<F> x, w, y;
+      lds_get(x, data + (size_t)lds_slot((uint32_t)(g * R + k)) * NW);
+      const size_t addr = out_addr(g, k);
+      tw2(w, tlo, thi, a.h, (uint32_t)a.T * (uint32_t)k * (uint32_t)(addr % S));
+      fe_mul(y, x, w);
+      fe_store_packed(dst + addr * F::N64, y);
+    }
+  } else if (scale) {
+    Fe<F> sc, t;
     fe_load_ref(t, scale);
     fe_to_int(sc, t);
-  } else {
-    fe_one(sc);
-  }
-  for (int e = tid; e < nel; e += NT) {
-    const int g = e % G, k = e / G;  // consecutive threads -> consecutive g (coalesced)
-    Fe<F> x;
-    lds_get(x, data + (size_t)lds_slot((uint32_t)(g * R + k)) * NW);
-    size_t addr;
-    if (!a.last) {
-      addr = hi_base + (size_t)k * S + g;
-      Fe<F> w, y;
-      if (a.otf) tw2(w, tlo, thi, a.h, (uint32_t)a.T * (uint32_t)k * (uint32_t)(addr % S));
-      else fe_load_ref(w, tab + ((size_t)k * S + (addr % S)) * F::N64);
-      fe_mul(y, x, w);
-      x = y;
-    } else {
-      addr = (a.P == 1) ? (size_t)k : nat_base + (size_t)(k0base + g) + (size_t)k * a.T;
-      // closing step: the lazily grown value (< 34p) back below 2p, as fe_store_ref's
-      // canonicalisation needs -- by the product with the scale (1/N) when an inverse's
-      // scale has no table to ride on, else by a product-free reduction
-      if (scale) {
-        Fe<F> y;
-        fe_mul(y, x, sc);
-        x = y;
-      } else {
-        fe_reduce_small(x);
-      }
+    for (int e = tid; e < nel; e += NT) {
+      const int g = e % G, k = e / G;
+      Fe<F> x, y;
+      lds_get(x, data + (size_t)lds_slot((uint32_t)(g * R + k)) * NW);
+      fe_mul(y, x, sc);
+      fe_store_ref(dst + out_addr(g, k) * F::N64, y);
     }
-    // a non-last pass's output is a product (< 2p < 2^256, both Fr moduli are below 2^255):
-    // stored packed but not canonicalised -- the next pass only multiplies and adds it
-    if (!a.last) fe_store_packed(dst + addr * F::N64, x);
-    else fe_store_ref(dst + addr * F::N64, x);
+  } else {
+    for (int e = tid; e < nel; e += NT) {
+      const int g = e % G, k = e / G;
+      Fe<F> x;
+      lds_get(x, data + (size_t)lds_slot((uint32_t)(g * R + k)) * NW);
+      fe_reduce_small(x);
+      fe_store_ref(dst + out_addr(g, k) * F::N64, x);
+    }
   }
 }
 
@@ -435,8 +457,9 @@ struct TwSet {
   size_t bytes = 0;
   uint64_t last_use = 0;
 };
-typedef std::tuple<int, int, int, uint64_t, uint64_t, uint64_t, uint64_t> TwKey;
-static std::map<TwKey, TwSet> g_tw;  // entries of device d are only touched under d's mutex
+// (context uid, m | first radix << 8, direction, generator, table cap)
+typedef std::tuple<int, int, int, uint64_t, uint64_t, uint64_t, uint64_t, size_t> TwKey;
+static std::map<TwKey, TwSet> g_tw;  // entries of context d are only touched under d's mutex
 static std::mutex g_tw_mu;          // guards the map structure itself
 static uint64_t g_tw_clock = 0;
 static const size_t TW_CACHE_LIMIT = (size_t)8 << 30;
@@ -447,7 +470,9 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
   using F = typename Cfg::Fd;
   using HF = typename Cfg::Fh;
   // the tables depend on the pass split too (the test hook can change it between calls)
-  TwKey key(dev.id * 2 + curve, m | (dig[0] << 8), inverse, gen_mont[0], gen_mont[1], gen_mont[2], gen_mont[3]);
+  const size_t table_max = ntt_table_max();
+  TwKey key(dev.uid * 2 + curve, m | (dig[0] << 8), inverse, gen_mont[0], gen_mont[1], gen_mont[2], gen_mont[3],
+            table_max);
   std::lock_guard<std::mutex> lock(g_tw_mu);
   auto it = g_tw.find(key);
   if (it != g_tw.end()) {
@@ -486,31 +511,38 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
     S >>= dig[p];
     words += ((size_t)1 << dig[p]) / 2 * el + el;
     words += ((size_t)1 << dig[p]) / 2 * (ITW_STRIDE / 2) + 2;
-    if (p < P - 1 && ((size_t)1 << dig[p]) * S <= ZK_NTT_TABLE_MAX) {
+    if (p < P - 1 && ((size_t)1 << dig[p]) * S <= table_max) {
       tab_words[p] = ((size_t)1 << dig[p]) * S * el;
       words += tab_words[p];
     }
     T <<= dig[p];
   }
-  // evict least-recently used sets beyond the cache limit
-  size_t total = words * 8;
-  for (auto &kv : g_tw)
-    if (std::get<0>(kv.first) / 2 == dev.id) total += kv.second.bytes;
-  while (total > TW_CACHE_LIMIT) {
+  // evict least-recently used sets of this context beyond the cache limit (and, when the
+  // device is out of memory, until the new set fits)
+  auto evict_one = [&]() -> bool {
     auto victim = g_tw.end();
     for (auto i2 = g_tw.begin(); i2 != g_tw.end(); ++i2)
-      if (std::get<0>(i2->first) / 2 == dev.id &&
+      if (std::get<0>(i2->first) / 2 == dev.uid &&
           (victim == g_tw.end() || i2->second.last_use < victim->second.last_use))
         victim = i2;
-    if (victim == g_tw.end()) break;
-    total -= victim->second.bytes;
+    if (victim == g_tw.end()) return false;
     ZK_CHECK(hipStreamSynchronize(dev.stream));
     ZK_CHECK(hipFree(victim->second.mem));
     g_tw.erase(victim);
+    return true;
+  };
+  for (;;) {
+    size_t total = words * 8;
+    for (auto &kv : g_tw)
+      if (std::get<0>(kv.first) / 2 == dev.uid) total += kv.second.bytes;
+    if (total <= TW_CACHE_LIMIT || !evict_one()) break;
   }
   TwSet ts;
   ts.bytes = words * 8;
-  ZK_CHECK(hipMalloc(&ts.mem, ts.bytes));
+  while (hipMalloc(&ts.mem, ts.bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    ZK_REQUIRE(evict_one(), "ntt: out of device memory for the twiddle tables");
+  }
   uint64_t *cur = ts.mem;
   auto take = [&](size_t w) { uint64_t *p = cur; cur += (w + 1) & ~size_t(1); return p; };
   uint64_t *tlo = take(((size_t)1 << h) * el);
@@ -583,7 +615,21 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   const size_t elbytes = (size_t)F::N64 * 8;
   size_t need = N * elbytes + (1 << 20);
   if (host_io) need += 2 * N * elbytes;
-  dev.arena.reserve(need);
+  if (!dev.arena.try_reserve(need)) {  // out of memory: drop the other cached twiddle sets
+    {
+      std::lock_guard<std::mutex> lock(g_tw_mu);
+      ZK_CHECK(hipStreamSynchronize(dev.stream));
+      for (auto it = g_tw.begin(); it != g_tw.end();) {
+        if (std::get<0>(it->first) / 2 == dev.uid && &it->second != &tw) {
+          ZK_CHECK(hipFree(it->second.mem));
+          it = g_tw.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    dev.arena.reserve(need);
+  }
   dev.arena.reset();
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
@@ -645,6 +691,18 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   if (host_io) ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
   stream_wait(dev, st);
   timer_collect(dev);
+}
+
+void ntt_release(Device &dev) {
+  std::lock_guard<std::mutex> lock(g_tw_mu);
+  for (auto it = g_tw.begin(); it != g_tw.end();) {
+    if (std::get<0>(it->first) / 2 == dev.uid) {
+      ZK_CHECK(hipFree(it->second.mem));
+      it = g_tw.erase(it);
+    } else {
+      ++it;
+    }
+  }
 }
 
 void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst, bool host_io,

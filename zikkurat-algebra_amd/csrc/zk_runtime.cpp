@@ -1,6 +1,9 @@
 // zk_runtime.cpp -- per-device context: stream, grow-only arena, pinned staging.
 #include "zk_runtime.hpp"
 #include <atomic>
+#include <chrono>
+#include <map>
+#include <thread>
 
 namespace zk {
 
@@ -10,15 +13,43 @@ namespace zk {
   abort();
 }
 
-void Arena::reserve(size_t bytes) {
-  if (bytes <= cap_) return;
+static std::atomic<size_t> g_arena_limit{0};
+void arena_set_limit(size_t bytes) { g_arena_limit.store(bytes); }
+
+bool Arena::try_reserve(size_t bytes) {
+  if (bytes <= cap_) return true;
+  const size_t limit = g_arena_limit.load();
+  if (limit && bytes > limit) return false;
   if (base_) ZK_CHECK(hipFree(base_));
   base_ = nullptr;
   cap_ = 0;
-  // grow geometrically to avoid re-allocation churn across sizes
+  // grow geometrically to avoid re-allocation churn across sizes; exactly `bytes` if the
+  // headroom does not fit
   size_t cap = bytes + bytes / 4;
-  ZK_CHECK(hipMalloc(&base_, cap));
+  if (limit && cap > limit) cap = limit;
+  if (hipMalloc(&base_, cap) != hipSuccess) {
+    (void)hipGetLastError();  // out-of-memory is not sticky: clear it
+    base_ = nullptr;
+    cap = bytes;
+    if (hipMalloc(&base_, cap) != hipSuccess) {
+      (void)hipGetLastError();
+      base_ = nullptr;
+      return false;
+    }
+  }
   cap_ = cap;
+  return true;
+}
+
+void Arena::reserve(size_t bytes) {
+  if (!try_reserve(bytes)) fatal("out of device memory for the call's working set", __FILE__, __LINE__);
+}
+
+void Arena::release() {
+  if (base_) ZK_CHECK(hipFree(base_));
+  base_ = nullptr;
+  cap_ = 0;
+  off_ = 0;
 }
 
 Arena::~Arena() {
@@ -34,30 +65,113 @@ void *Device::host_staging(size_t bytes) {
   return pinned;
 }
 
+void Device::release_memory() {
+  arena.release();
+  if (pinned) ZK_CHECK(hipHostFree(pinned));
+  pinned = nullptr;
+  pinned_cap = 0;
+}
+
 static std::mutex g_devices_mu;
-static std::vector<Device *> g_devices;
+static std::map<std::pair<int, int>, Device *> g_devices;  // (id, slot) -> context (never freed)
+
+Device &device_context(int id, int slot) {
+  std::lock_guard<std::mutex> lock(g_devices_mu);
+  auto it = g_devices.find({id, slot});
+  if (it != g_devices.end()) return *it->second;
+  int prev = 0;
+  ZK_CHECK(hipGetDevice(&prev));
+  if (prev != id) ZK_CHECK(hipSetDevice(id));
+  Device *d = new Device();
+  d->id = id;
+  d->slot = slot;
+  d->uid = (int)g_devices.size();
+  ZK_CHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  if (prev != id) ZK_CHECK(hipSetDevice(prev));
+  g_devices[{id, slot}] = d;
+  return *d;
+}
 
 Device &current_device() {
   int id = 0;
   ZK_CHECK(hipGetDevice(&id));
+  return device_context(id, 0);
+}
+
+std::vector<Device *> all_devices() {
   std::lock_guard<std::mutex> lock(g_devices_mu);
-  if ((int)g_devices.size() <= id) g_devices.resize(id + 1, nullptr);
-  if (!g_devices[id]) {
-    Device *d = new Device();
-    d->id = id;
-    ZK_CHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-    g_devices[id] = d;
+  std::vector<Device *> v;
+  for (auto &kv : g_devices) v.push_back(kv.second);
+  return v;
+}
+
+static std::mutex g_set_mu;
+static std::vector<int> g_set;
+static bool g_set_init = false;
+
+static int device_count_or_zero() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
   }
-  return *g_devices[id];
+  return n;
+}
+
+std::vector<int> device_set() {
+  std::lock_guard<std::mutex> lock(g_set_mu);
+  if (!g_set_init) {
+    g_set_init = true;
+    const char *env = getenv("ZKG_DEVICES");
+    if (env && *env) {
+      const int count = device_count_or_zero();
+      std::vector<int> v;
+      if (std::string(env) == "all") {
+        for (int i = 0; i < count; i++) v.push_back(i);
+      } else {
+        const char *p = env;
+        while (*p) {
+          char *end = nullptr;
+          const long id = strtol(p, &end, 10);
+          if (end == p || id < 0 || id >= count) {
+            fprintf(stderr, "[zkalgebra_gpu] ZKG_DEVICES=%s: invalid device list, ignored\n", env);
+            v.clear();
+            break;
+          }
+          v.push_back((int)id);
+          p = *end == ',' ? end + 1 : end;
+        }
+      }
+      g_set = v;
+    }
+  }
+  return g_set;
+}
+
+int set_device_set(const int *ids, int n) {
+  const int count = device_count_or_zero();
+  for (int i = 0; i < n; i++)
+    if (ids[i] < 0 || ids[i] >= count) return -1;
+  std::lock_guard<std::mutex> lock(g_set_mu);
+  g_set.assign(ids, ids + (n > 0 ? n : 0));
+  g_set_init = true;
+  return 0;
 }
 
 void stream_wait(Device &dev, hipStream_t st) {
   if (!dev.sync_ev) ZK_CHECK(hipEventCreateWithFlags(&dev.sync_ev, hipEventDisableTiming));
   ZK_CHECK(hipEventRecord(dev.sync_ev, st));
+  // spin for the first 0.2 ms (the wake-up latency of a blocking wait is ~0.1 ms, which the
+  // short calls would pay in full), then yield, and beyond 2 ms sleep 20 us between polls so
+  // long calls (host-buffer copies, large transforms) do not pin a host core
+  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipEventQuery(dev.sync_ev);
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) ZK_CHECK(e);
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (us > 2000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else if (us > 200) std::this_thread::yield();
   }
 }
 
@@ -100,11 +214,7 @@ void timer_collect(Device &dev) {
 }
 
 void timer_reset_all() {
-  std::vector<Device *> devs;
-  {
-    std::lock_guard<std::mutex> lock(g_devices_mu);
-    devs = g_devices;
-  }
+  const std::vector<Device *> devs = all_devices();
   for (Device *d : devs)
     if (d) {
       std::lock_guard<std::mutex> lock(d->mu);
@@ -114,11 +224,7 @@ void timer_reset_all() {
 }
 
 void timer_read_all(double *total_ms, long *launches) {
-  std::vector<Device *> devs;
-  {
-    std::lock_guard<std::mutex> lock(g_devices_mu);
-    devs = g_devices;
-  }
+  const std::vector<Device *> devs = all_devices();
   double t = 0;
   long n = 0;
   for (Device *d : devs)

@@ -32,9 +32,15 @@ namespace zk {
   } while (0)
 
 // Bump allocator over a grow-only device buffer. reset() at the start of every call.
+// try_reserve() reports an allocation failure (hipMalloc out of memory, or the test hook's
+// cap, arena_set_limit) instead of aborting, so callers can degrade (smaller MSM window
+// groups, dropping cached NTT twiddles) before giving up; release() returns the memory.
 class Arena {
  public:
-  void reserve(size_t bytes);  // grows (re-allocates) only when larger than current
+  void reserve(size_t bytes);      // try_reserve or fatal
+  bool try_reserve(size_t bytes);  // grows (re-allocates) only when larger than current
+  void release();                  // frees the buffer (the next reserve re-allocates)
+  size_t capacity() const { return cap_; }
   void reset() { off_ = 0; }
   void rewind(size_t off) { off_ = off; }  // release everything taken after used() == off
   template <class T>
@@ -66,8 +72,17 @@ struct KernelTimer {
   long launches = 0;
 };
 
+// test hook: device bytes one arena may hold (0: unlimited), to exercise the degrade paths
+void arena_set_limit(size_t bytes);
+
+// One device context: a stream, an arena and pinned staging, guarded by `mu`.  Context
+// (id, 0) is the one the C-ABI entry points use on the calling thread's device; contexts
+// (id, k > 0) exist when the device set (below) lists device id more than once, so that
+// logical shards on one physical device run on streams and arenas of their own.
 struct Device {
-  int id = 0;
+  int id = 0;    // physical HIP device
+  int slot = 0;  // context index on that device
+  int uid = 0;   // unique per context (keys per-context caches)
   hipStream_t stream = nullptr;
   Arena arena;
   std::mutex mu;
@@ -77,6 +92,7 @@ struct Device {
   void *host_staging(size_t bytes);
   KernelTimer timer;
   hipEvent_t sync_ev = nullptr;  // stream_wait's marker
+  void release_memory();         // arena + pinned staging (caller holds mu, stream idle)
 };
 
 // Wait for everything enqueued on st by spinning on an event (caller holds dev.mu): the
@@ -84,8 +100,20 @@ struct Device {
 // a blocking stream synchronisation (up to ~0.1 ms measured in the MSM's export phase).
 void stream_wait(Device &dev, hipStream_t st);
 
-// The device of the calling thread (hipGetDevice), lazily initialised.
+// The device of the calling thread (hipGetDevice), lazily initialised: context (id, 0).
 Device &current_device();
+// Context (id, slot), created on first use (its stream lives on device id).
+Device &device_context(int id, int slot);
+// Every context created so far (for zkg_release).
+std::vector<Device *> all_devices();
+
+// Device set of the host-buffer MSM entry points: the pairs are split into contiguous
+// chunks, one per listed device (a device may be listed more than once: one context per
+// occurrence), computed concurrently, and the partial sums added in list order.  Empty or
+// one entry: the calling thread's device only.  Initialised from the environment variable
+// ZKG_DEVICES ("all", or a comma-separated list of device ids) on first use.
+std::vector<int> device_set();
+int set_device_set(const int *ids, int n);  // 0 on success, -1 for an invalid id
 
 // kernel timer (caller holds dev.mu for begin/end/collect)
 void timer_set_enabled(bool on);

@@ -57,9 +57,11 @@ EXTENSION_SYMBOLS = [
     "zkg_memcpy_htod", "zkg_memcpy_dtoh", "zkg_device_synchronize", "zkg_g1_msm_device", "zkg_ntt_device",
     "zkg_g1_proj_add", "zkg_g1_proj_normalize", "zkg_g1_proj_to_affine", "zkg_gen_fr", "zkg_gen_g1_points",
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
-    "zkg_field_mul_rate", "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
+    "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
     "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
-    "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_ntt_set_max_radix",
+    "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_ntt_set_max_radix", "zkg_ntt_set_table_max",
+    "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
+    "zkg_release",
 ]
 
 _lib = None
@@ -86,8 +88,12 @@ def load():
         lib.zkg_gen_g1_points.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, U64P]
         lib.zkg_timer_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]
         lib.zkg_msm_set_group_limit.argtypes = [ctypes.c_size_t]
-        lib.zkg_field_mul_rate.restype = ctypes.c_double
-        lib.zkg_field_mul_rate.argtypes = [ctypes.c_int]
+        lib.zkg_ntt_set_table_max.argtypes = [ctypes.c_size_t]
+        lib.zkg_arena_set_limit.argtypes = [ctypes.c_size_t]
+        lib.zkg_msm_workspace_bytes.restype = ctypes.c_size_t
+        lib.zkg_msm_workspace_bytes.argtypes = [ctypes.c_int] * 7
+        lib.zkg_set_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        lib.zkg_get_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         for c in CURVES:
             for o in ("is_valid", "is_zero", "is_one", "is_equal"):
                 getattr(lib, f"{c}_arr_mont_{o}").restype = ctypes.c_uint8
@@ -207,9 +213,8 @@ def msm_proj(curve, coeffs, proj_points):
     """Proj.msmProj cs gs = msm cs (batchToAffine gs) (G1/Proj.hs:222-223)."""
     if proj_points.ndim != 2 or proj_points.shape[1] != 3 * NLIMBS_P[curve]:
         raise ValueError("msm: incompatible array dimensions")
-    aff = np.stack([g1_to_affine(curve, p) for p in proj_points]) if len(proj_points) else \
-        np.zeros((0, 2 * NLIMBS_P[curve]), dtype=np.uint64)
-    return msm(curve, coeffs, np.ascontiguousarray(aff))
+    # batchToAffine on the GPU (<C>_G1_proj_batch_to_affine, Montgomery's trick), as msmProj does
+    return msm(curve, coeffs, batch_to_affine(curve, proj_points))
 
 
 def g2_msm(curve, coeffs, points, std=False, affine=False):
@@ -557,12 +562,43 @@ def ntt_device(curve, m, gen, d_src, d_dst, inverse=False):
                           d_dst.ptr)
 
 
-FIELD_ID = {("bn128", "fp"): 0, ("bn128", "fr"): 1, ("bls12_381", "fp"): 2, ("bls12_381", "fr"): 3}
+def ntt_set_table_max(entries):
+    """test hook: inter-pass twiddle entries above which NTT passes compute twiddles on the fly (0: default)"""
+    load().zkg_ntt_set_table_max(int(entries))
 
 
-def field_mul_rate(curve, field):
-    """measured Montgomery products/s of the device field engine (VALU roofline probe)"""
-    return load().zkg_field_mul_rate(FIELD_ID[(curve, field)])
+def arena_set_limit(nbytes):
+    """test hook: cap on one working-set arena's device bytes (0: unlimited)"""
+    load().zkg_arena_set_limit(int(nbytes))
+
+
+def msm_last_groups():
+    return load().zkg_msm_last_groups()
+
+
+def msm_workspace_bytes(curve, n, nlimbs=4, mont=True, host_inputs=True, window=0, groups=1):
+    """device bytes of one G1 MSM's working set with its windows in `groups` passes"""
+    return load().zkg_msm_workspace_bytes(CURVE_ID[curve], n, nlimbs, 1 if mont else 0, 1 if host_inputs else 0,
+                                          window, groups)
+
+
+def set_devices(ids):
+    """device set of the host-buffer MSM entries (zkg_set_devices); [] = calling thread's device"""
+    ids = list(ids)
+    arr = (ctypes.c_int * max(1, len(ids)))(*ids)
+    if load().zkg_set_devices(arr, len(ids)) != 0:
+        raise ValueError(f"set_devices: invalid device id in {ids}")
+
+
+def get_devices():
+    arr = (ctypes.c_int * 64)()
+    n = load().zkg_get_devices(arr, 64)
+    return list(arr[:min(n, 64)])
+
+
+def release():
+    """free every device buffer the library caches (zkg_release)"""
+    load().zkg_release()
 
 
 def timer(enable=None, reset=False):

@@ -140,3 +140,32 @@ def test_variable_window_edges(gpu, oracle, curve, window):
     pts = gpu.gen_points(curve, 32, n)
     want = oracle.normalize(curve, oracle.msm(curve, sc, pts, mont=False, out="proj"))
     assert np.array_equal(gpu.msm_variable(curve, sc, pts, window), want)
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8], indirect=True)
+@pytest.mark.parametrize("curve", CURVES)
+def test_ntt_host_io_spread(gpu, curve, shards):
+    """<C>_poly_mont_ntt_{forward,inverse} with a device set: the transform runs on the first
+    listed device, the host copies are split over every listed one (peer / device-to-device
+    copies to the compute device) -- against the reference's digests at 2^20 and the unsharded
+    results at 2^16 and 2^17 (uneven chunks), in place and out of place"""
+    import hashlib
+    from golden_io import ntt_patterns_golden
+    cases = ntt_patterns_golden()["cases"]
+    sg = gpu.get_fft_subgroup(curve, 20)
+    x = gpu.gen_fr(curve, 0x5A4B0003, 1 << 20)
+    for inverse, key in ((False, "forward"), (True, "inverse")):
+        y = gpu.inverse_ntt(sg, x) if inverse else gpu.forward_ntt(sg, x)
+        assert hashlib.sha256(y.tobytes()).hexdigest() == cases[f"{curve}/random/m20/{key}"]["sha256"]
+    for m in (16, 17):
+        sgm = gpu.get_fft_subgroup(curve, m)
+        z = gpu.gen_fr(curve, 0x51 + m, 1 << m)
+        f = gpu.forward_ntt(sgm, z)
+        gpu.set_devices([])
+        want = gpu.forward_ntt(sgm, z)
+        gpu.set_devices([0] * shards)
+        assert np.array_equal(f, want)
+        buf = f.copy()
+        lib = gpu.load()
+        getattr(lib, f"{curve}_poly_mont_ntt_inverse")(m, gpu._p(sgm.gen_array()), gpu._p(buf), gpu._p(buf))
+        assert np.array_equal(buf, z)  # in place (src == tgt)

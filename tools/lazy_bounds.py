@@ -149,6 +149,19 @@ class Field:
         self._columns(lambda k: sum(a.lim[i] * b.lim[k - i] for i in range(max(0, k - N + 1), min(k, N - 1) + 1)), what)
         return self._prod_out((a.val - 1) * (b.val - 1) + 1, what)
 
+    def mulk(self, a, b, what="mulk"):
+        """fe_mulk (Karatsuba column sums on the 14-limb field, schoolbook otherwise): the columns
+        equal the schoolbook ones; the split differences a_lo - a_hi, b_hi - b_lo are int32, so
+        every limb must be < 2^31"""
+        if self.N == 14:
+            self.need(all(l < (1 << 31) for l in a.lim + b.lim), f"{what}: limb >= 2^31 (int32 differences)")
+        return self.mul(a, b, what)
+
+    def mul2k(self, a, b, c, d, what="mul2k"):
+        if self.N == 14:
+            self.need(all(l < (1 << 31) for l in a.lim + b.lim + c.lim + d.lim), f"{what}: limb >= 2^31")
+        return self.mul2(a, b, c, d, what)
+
     def mul2(self, a, b, c, d, what="mul2"):
         N = self.N
         for x in (a, b, c, d):
@@ -316,28 +329,28 @@ def dbl(F, pt, tag):
 
 
 def madd_lazy14(F):
-    """zk_curve.hpp xyzz_add_aff_lazy (BLS12-381 Fp, 14 x 28)"""
+    """zk_curve.hpp xyzz_add_aff_lazy (BLS12-381 Fp, 14 x 28; products on Karatsuba column sums)"""
     p, tag = F.p, "xyzz_add_aff_lazy"
     acc = bucket_form(F)
     x, y = affine_input(F)
-    t = F.mul(x, acc["ZZ"], tag + " U2")
+    t = F.mulk(x, acc["ZZ"], tag + " U2")
     P = F.sub_lazy(t, acc["X"], 16, 1, tag + " P")
-    t = F.mul(y, acc["ZZZ"], tag + " S2")
+    t = F.mulk(y, acc["ZZZ"], tag + " S2")
     R = F.sub_lazy(t, acc["Y"], 8, 1, tag + " R")
     PP = F.sqr(P, tag + " PP")
     RR = F.sqr(R, tag + " RR")
     F.is_zero_ok(PP, tag + " PP")
     F.is_zero_ok(RR, tag + " RR")
     in_form(F, dbl_aff(F, x, y, tag + " (P = R = 0 branch) dbl_aff"), tag + " doubling branch")
-    PPP = F.mul(P, PP, tag + " PPP")
-    Q = F.mul(acc["X"], PP, tag + " Q")
+    PPP = F.mulk(P, PP, tag + " PPP")
+    Q = F.mulk(acc["X"], PP, tag + " Q")
     t = F.sub_lazy(RR, PPP, 4, 1, tag + " RR-PPP")
     q2 = F.add_lazy(Q, Q, tag + " 2Q")
     X3 = F.norm(F.sub_lazy(t, q2, 8, 2, tag + " X3"), tag + " X3")
     t = F.sub_lazy(Q, X3, 16, 1, tag + " Q-X3")
     ny = F.sub_lazy(F.zero(), acc["Y"], 6, 1, tag + " 6p-Y1")
-    Y3 = F.mul2(R, t, ny, PPP, tag + " Y3")
-    out = {"X": X3, "Y": Y3, "ZZ": F.mul(acc["ZZ"], PP, tag + " ZZ3"), "ZZZ": F.mul(acc["ZZZ"], PPP, tag + " ZZZ3")}
+    Y3 = F.mul2k(R, t, ny, PPP, tag + " Y3")
+    out = {"X": X3, "Y": Y3, "ZZ": F.mulk(acc["ZZ"], PP, tag + " ZZ3"), "ZZZ": F.mulk(acc["ZZZ"], PPP, tag + " ZZZ3")}
     in_form(F, out, tag)
     F.log.append(f"{tag}: P < {F.units(P):.1f} p, R < {F.units(R):.1f} p, X3 < {F.units(X3):.1f} p, "
                  f"Y3 < {F.units(Y3):.2f} p (R'/p = {F.Rp / p:.0f})")
@@ -376,18 +389,18 @@ def add_lazy(F):
     tag = "xyzz_add_lazy"
     W9 = F.N == 9
     a, b = bucket_form(F), bucket_form(F)
-    U1 = F.mul(a["X"], b["ZZ"], tag + " U1")
-    t = F.mul(b["X"], a["ZZ"], tag + " U2")
+    U1 = F.mulk(a["X"], b["ZZ"], tag + " U1")
+    t = F.mulk(b["X"], a["ZZ"], tag + " U2")
     P = F.norm(F.sub_lazy(t, U1, 3, 1, tag + " P")) if W9 else F.sub_lazy(t, U1, 4, 1, tag + " P")
-    S1 = F.mul(a["Y"], b["ZZZ"], tag + " S1")
-    t = F.mul(b["Y"], a["ZZZ"], tag + " S2")
+    S1 = F.mulk(a["Y"], b["ZZZ"], tag + " S1")
+    t = F.mulk(b["Y"], a["ZZZ"], tag + " S2")
     R = F.norm(F.sub_lazy(t, S1, 3, 1, tag + " R")) if W9 else F.sub_lazy(t, S1, 4, 1, tag + " R")
     PP, RR = F.sqr(P, tag + " PP"), F.sqr(R, tag + " RR")
     F.is_zero_ok(PP, tag + " PP")
     F.is_zero_ok(RR, tag + " RR")
     in_form(F, dbl(F, b, tag + " dbl"), tag + " doubling branch")
-    PPP = F.mul(P, PP, tag + " PPP")
-    Q = F.mul(U1, PP, tag + " Q")
+    PPP = F.mulk(P, PP, tag + " PPP")
+    Q = F.mulk(U1, PP, tag + " Q")
     q2 = F.add_lazy(Q, Q)
     if W9:
         t = F.sub_lazy(RR, PPP, 3, 1, tag)
@@ -399,10 +412,10 @@ def add_lazy(F):
         X3 = F.norm(F.sub_lazy(t, q2, 8, 2, tag + " X3"))
         t = F.sub_lazy(Q, X3, 16, 1, tag + " Q-X3")
         ny = F.sub_lazy(F.zero(), S1, 4, 1, tag + " 4p-S1")
-    zz = F.mul(a["ZZ"], b["ZZ"])
-    zzz = F.mul(a["ZZZ"], b["ZZZ"])
-    Y3 = F.mul2(R, t, ny, PPP, tag + " Y3")
-    out = {"X": X3, "Y": Y3, "ZZ": F.mul(zz, PP), "ZZZ": F.mul(zzz, PPP)}
+    zz = F.mulk(a["ZZ"], b["ZZ"])
+    zzz = F.mulk(a["ZZZ"], b["ZZZ"])
+    Y3 = F.mul2k(R, t, ny, PPP, tag + " Y3")
+    out = {"X": X3, "Y": Y3, "ZZ": F.mulk(zz, PP), "ZZZ": F.mulk(zzz, PPP)}
     in_form(F, out, tag)
     F.log.append(f"{tag}: P, R < {F.units(P):.1f} p, X3 < {F.units(X3):.1f} p, Y3 < {F.units(Y3):.2f} p")
 

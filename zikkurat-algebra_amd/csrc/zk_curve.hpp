@@ -159,14 +159,21 @@ __device__ __forceinline__ void xyzz_add_aff(Xyzz<F> &acc, const Aff<F> &a) {
 //   Y3 = (R t + (6p - Y1) PPP) / R' < 1.06p
 // Column sums in fe_mul2 (R t: limbs < 2^29.6 each; (6p - Y1): < 2^29.6) stay < 2^64.  (The
 // once-documented Y < 6p would break 6p - Y1's top-limb borrow; every producer gives Y < 1.06p.)
+#ifndef ZK_KARA_MADD
+#define ZK_KARA_MADD 1  // the madd's products on Karatsuba column sums (fe_mulk); 0: schoolbook
+#endif
+template <class F>
+__device__ __forceinline__ void madd_mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  if constexpr (ZK_KARA_MADD) fe_mulk(r, a, b); else fe_mul(r, a, b);
+}
 template <class F>
 __device__ __forceinline__ void xyzz_add_aff_lazy(Xyzz<F> &acc, const Aff<F> &a) {
   static_assert(F::N == 14 && F::RB == 28, "lazy madd bounds are derived for the 14 x 28-bit field");
   if (xyzz_is_inf(acc)) { xyzz_from_aff(acc, a); return; }
   Fe<F> P, R, PP, RR, t;
-  fe_mul(t, a.x, acc.ZZ);                 // U2
+  madd_mul(t, a.x, acc.ZZ);               // U2
   fe_sub_lazy<F, 16, 1>(P, t, acc.X);     // P = U2 - X1
-  fe_mul(t, a.y, acc.ZZZ);                // S2
+  madd_mul(t, a.y, acc.ZZZ);              // S2
   fe_sub_lazy<F, 8, 1>(R, t, acc.Y);      // R = S2 - Y1
   fe_sqr(PP, P);
   fe_sqr(RR, R);
@@ -176,8 +183,8 @@ __device__ __forceinline__ void xyzz_add_aff_lazy(Xyzz<F> &acc, const Aff<F> &a)
     return;
   }
   Fe<F> PPP, Q, X3, q2;
-  fe_mul(PPP, P, PP);
-  fe_mul(Q, acc.X, PP);
+  madd_mul(PPP, P, PP);
+  madd_mul(Q, acc.X, PP);
   fe_sub_lazy<F, 4, 1>(t, RR, PPP);       // RR - PPP
   fe_add_lazy(q2, Q, Q);
   fe_sub_lazy<F, 8, 2>(X3, t, q2);        // - 2Q
@@ -185,10 +192,11 @@ __device__ __forceinline__ void xyzz_add_aff_lazy(Xyzz<F> &acc, const Aff<F> &a)
   fe_sub_lazy<F, 16, 1>(t, Q, X3);        // Q - X3
   Fe<F> ny;
   fe_sub_lazy<F, 6, 1>(ny, Fe<F>{}, acc.Y);  // 6p - Y1 (acc.Y < 2p, normalised)
-  fe_mul2(acc.Y, R, t, ny, PPP);          // Y3 = R (Q - X3) - Y1 PPP
+  if constexpr (ZK_KARA_MADD) fe_mul2k(acc.Y, R, t, ny, PPP);  // Y3 = R (Q - X3) - Y1 PPP
+  else fe_mul2(acc.Y, R, t, ny, PPP);
   acc.X = X3;
-  fe_mul(acc.ZZ, acc.ZZ, PP);
-  fe_mul(acc.ZZZ, acc.ZZZ, PPP);
+  madd_mul(acc.ZZ, acc.ZZ, PP);
+  madd_mul(acc.ZZZ, acc.ZZZ, PPP);
 }
 // The same for the 254-bit base field (9 x 29-bit limbs, R'/p ~ 2^7.4: too little headroom to
 // keep X lazily, so X3 is brought below 2p by the product-free fe_reduce_small).  The
@@ -286,6 +294,15 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
 //   381-bit: P = U2 + 4p - U1 < 6p, R = S2 + 4p - S1 < 6p, X3 < 14p as in the madd,
 //            Y3: R (Q + 16p - X3) + (4p - S1) PPP < (6 * 18 + 4 * 2) p^2 < p R' (R'/p > 2^11)
 //   254-bit: as xyzz_add_aff_lazy9 with U1, S1 (< 2p) in place of X1, Y1
+#ifndef ZK_KARA_ADD
+// the 381-bit lazy full add's products on Karatsuba column sums (1) or schoolbook (0): no
+// measurable difference in the Y sums / stitch (profiles/r03b_karatsuba_ab.txt), schoolbook kept
+#define ZK_KARA_ADD 0
+#endif
+template <class F>
+__device__ __forceinline__ void add_mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  if constexpr (ZK_KARA_ADD) fe_mulk(r, a, b); else fe_mul(r, a, b);
+}
 template <class F>
 __device__ __forceinline__ void xyzz_add_lazy(Xyzz<F> &acc, const Xyzz<F> &b) {
   static_assert(F::N == 14 || (F::N == 9 && F::RB == 29), "lazy bounds derived for the G1 base fields");
@@ -293,12 +310,12 @@ __device__ __forceinline__ void xyzz_add_lazy(Xyzz<F> &acc, const Xyzz<F> &b) {
   if (xyzz_is_inf(b)) return;
   if (xyzz_is_inf(acc)) { acc = b; return; }
   Fe<F> U1, S1, P, R, PP, RR, t;
-  fe_mul(U1, acc.X, b.ZZ);
-  fe_mul(t, b.X, acc.ZZ);                             // U2
+  add_mul(U1, acc.X, b.ZZ);
+  add_mul(t, b.X, acc.ZZ);                            // U2
   if constexpr (W9) { fe_sub_lazy<F, 3, 1>(P, t, U1); fe_norm(P); }
   else fe_sub_lazy<F, 4, 1>(P, t, U1);                // P = U2 - U1
-  fe_mul(S1, acc.Y, b.ZZZ);
-  fe_mul(t, b.Y, acc.ZZZ);                            // S2
+  add_mul(S1, acc.Y, b.ZZZ);
+  add_mul(t, b.Y, acc.ZZZ);                           // S2
   if constexpr (W9) { fe_sub_lazy<F, 3, 1>(R, t, S1); fe_norm(R); }
   else fe_sub_lazy<F, 4, 1>(R, t, S1);                // R = S2 - S1
   fe_sqr(PP, P);
@@ -309,8 +326,8 @@ __device__ __forceinline__ void xyzz_add_lazy(Xyzz<F> &acc, const Xyzz<F> &b) {
     return;
   }
   Fe<F> PPP, Q, X3, q2, ny;
-  fe_mul(PPP, P, PP);
-  fe_mul(Q, U1, PP);
+  add_mul(PPP, P, PP);
+  add_mul(Q, U1, PP);
   fe_add_lazy(q2, Q, Q);
   if constexpr (W9) {
     fe_sub_lazy<F, 3, 1>(t, RR, PPP);
@@ -329,12 +346,13 @@ __device__ __forceinline__ void xyzz_add_lazy(Xyzz<F> &acc, const Xyzz<F> &b) {
     fe_sub_lazy<F, 4, 1>(ny, Fe<F>{}, S1);            // 4p - S1
   }
   Fe<F> zz, zzz;
-  fe_mul(zz, acc.ZZ, b.ZZ);
-  fe_mul(zzz, acc.ZZZ, b.ZZZ);
-  fe_mul2(acc.Y, R, t, ny, PPP);                      // Y3 = R (Q - X3) - S1 PPP
+  add_mul(zz, acc.ZZ, b.ZZ);
+  add_mul(zzz, acc.ZZZ, b.ZZZ);
+  if constexpr (ZK_KARA_ADD) fe_mul2k(acc.Y, R, t, ny, PPP);  // Y3 = R (Q - X3) - S1 PPP
+  else fe_mul2(acc.Y, R, t, ny, PPP);
   acc.X = X3;
-  fe_mul(acc.ZZ, zz, PP);
-  fe_mul(acc.ZZZ, zzz, PPP);
+  add_mul(acc.ZZ, zz, PP);
+  add_mul(acc.ZZZ, zzz, PPP);
 }
 // the Y sums' addition: lazy for the G1 base fields, exact for Fp2
 template <class F>

@@ -226,6 +226,107 @@ __device__ __forceinline__ void fe_mul2(Fe<F> &r, const Fe<F> &a, const Fe<F> &b
   for (int i = 0; i < N; i++) r.v[i] = o[i];
 }
 
+// ---- one Karatsuba level on the a*b part (even N; used for the 14-limb 381-bit field):
+//   a b = z0 + (z0 + z2 + z1') 2^(H RB) + z2 2^(2 H RB),  H = N/2,
+//   z0 = a_lo b_lo, z2 = a_hi b_hi, z1' = (a_lo - a_hi)(b_hi - b_lo)  (signed 32-bit differences,
+//   v_mad_i64_i32), so 3 H^2 limb products instead of N^2.  Column k of a b (kara_cols) equals
+// the schoolbook column sum exactly, so the interleaved REDC (redc_cols) sees the same column
+// values and bounds as fe_mul (tools/lazy_bounds.py); the middle columns are formed in
+// wrapping u64 arithmetic (the true value, a_lo b_hi + a_hi b_lo, is >= 0 and < 2^64).
+// Static A/B (tools/experiments/kara_isa.hip): 436 vs 472 issue slots per 381-bit product.
+template <class F>
+__device__ __forceinline__ void kara_cols(uint64_t (&T)[2 * F::N - 1], const Fe<F> &a, const Fe<F> &b,
+                                          bool accumulate) {
+  constexpr int N = F::N, H = N / 2;
+  static_assert(N % 2 == 0, "Karatsuba split needs an even limb count");
+  int32_t da[H], db[H];
+#pragma unroll
+  for (int i = 0; i < H; i++) {
+    da[i] = (int32_t)a.v[i] - (int32_t)a.v[i + H];
+    db[i] = (int32_t)b.v[i + H] - (int32_t)b.v[i];
+  }
+  uint64_t z0[2 * H - 1], z2[2 * H - 1], mid[2 * H - 1];
+#pragma unroll
+  for (int k = 0; k < 2 * H - 1; k++) {
+    uint64_t s0 = 0, s2 = 0;
+#pragma unroll
+    for (int i = 0; i < H; i++) {
+      const int j = k - i;
+      if (j < 0 || j >= H) continue;
+      s0 += (uint64_t)a.v[i] * b.v[j];
+      s2 += (uint64_t)a.v[i + H] * b.v[j + H];
+    }
+    z0[k] = s0;
+    z2[k] = s2;
+    uint64_t s1 = s0 + s2;
+#pragma unroll
+    for (int i = 0; i < H; i++) {
+      const int j = k - i;
+      if (j < 0 || j >= H) continue;
+      s1 += (uint64_t)((int64_t)da[i] * (int64_t)db[j]);
+    }
+    mid[k] = s1;
+  }
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint64_t t = accumulate ? T[k] : 0;
+    if (k < 2 * H - 1) t += z0[k];
+    if (k >= H && k - H < 2 * H - 1) t += mid[k - H];
+    if (k >= 2 * H && k - 2 * H < 2 * H - 1) t += z2[k - 2 * H];
+    T[k] = t;
+  }
+}
+// Montgomery reduction of product-scanning column sums T (the m*p part interleaved as in fe_mul)
+template <class F>
+__device__ __forceinline__ void redc_cols(Fe<F> &r, const uint64_t (&T)[2 * F::N - 1]) {
+  constexpr int N = F::N;
+  uint32_t m[N], o[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    acc += T[k];
+#pragma unroll
+    for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * F::p(k - i);
+    m[k] = ((uint32_t)acc * F::MINV) & F::MASK;
+    acc += (uint64_t)m[k] * F::p(0);
+    acc >>= F::RB;
+  }
+#pragma unroll
+  for (int k = N; k < 2 * N - 1; k++) {
+    acc += T[k];
+#pragma unroll
+    for (int i = k - N + 1; i < N; i++) acc += (uint64_t)m[i] * F::p(k - i);
+    o[k - N] = (uint32_t)acc & F::MASK;
+    acc >>= F::RB;
+  }
+  o[N - 1] = (uint32_t)acc;
+#pragma unroll
+  for (int i = 0; i < N; i++) r.v[i] = o[i];
+}
+// the product / shared-reduction pair with the Karatsuba column sums (14-limb field), the
+// schoolbook ones otherwise
+template <class F>
+__device__ __forceinline__ void fe_mulk(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  if constexpr (F::N == 14) {
+    uint64_t T[2 * F::N - 1];
+    kara_cols(T, a, b, false);
+    redc_cols(r, T);
+  } else {
+    fe_mul(r, a, b);
+  }
+}
+template <class F>
+__device__ __forceinline__ void fe_mul2k(Fe<F> &r, const Fe<F> &a, const Fe<F> &b, const Fe<F> &c, const Fe<F> &d) {
+  if constexpr (F::N == 14) {
+    uint64_t T[2 * F::N - 1];
+    kara_cols(T, a, b, false);
+    kara_cols(T, c, d, true);
+    redc_cols(r, T);
+  } else {
+    fe_mul2(r, a, b, c, d);
+  }
+}
+
 // squaring: off-diagonal products once, doubled (saves ~N^2/2 mads)
 template <class F>
 __device__ __forceinline__ void fe_sqr(Fe<F> &r, const Fe<F> &a) {

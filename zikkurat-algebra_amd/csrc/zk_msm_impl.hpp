@@ -186,15 +186,18 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *tmp
 // sorted by bin there, so every bin's run leaves as consecutive lanes' stores.
 template <bool SCATTER>
 __global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig, int n, int M, int s, int nbins,
-                                                uint32_t *__restrict__ cnt, uint32_t *__restrict__ tmpv,
-                                                uint16_t *__restrict__ tmpf) {
+                                                int W, int NS, uint32_t *__restrict__ cnt,
+                                                uint32_t *__restrict__ tmpv, uint16_t *__restrict__ tmpf) {
   __shared__ uint32_t hist[MSM_COARSE_BINS], lofs[MSM_COARSE_BINS], gcur[MSM_COARSE_BINS], scan_tmp[256];
   __shared__ uint32_t sv[SORT_CHUNK], sk[SORT_CHUNK];
-  const uint32_t w = blockIdx.y, g = blockIdx.x, nwg = gridDim.x;
+  // virtual window wv = split * W + window: the split's points [n h / NS, n (h+1) / NS) of the window
+  const uint32_t wv = blockIdx.y, g = blockIdx.x, nwg = gridDim.x;
+  const uint32_t w = wv % (uint32_t)W, h = wv / (uint32_t)W;
   const int t = threadIdx.x;
-  const int e0 = (int)g * M, e1 = min(n, e0 + M);
+  const int plo = (int)((int64_t)n * h / NS), phi = (int)((int64_t)n * (h + 1) / NS);
+  const int e0 = plo + (int)g * M, e1 = min(phi, e0 + M);
   const uint32_t *d = dig + (size_t)w * n;
-  uint32_t *cw = cnt + (size_t)w * nbins * nwg + g;
+  uint32_t *cw = cnt + (size_t)wv * nbins * nwg + g;
   if (!SCATTER) {
     if (w == 0 && g == 0 && t == 0) cnt[(size_t)gridDim.y * nbins * nwg] = 0;  // the scan's total slot
     for (int b = t; b < nbins; b += 256) hist[b] = 0;
@@ -338,15 +341,16 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
     k_accum(const uint32_t *__restrict__ points, const uint32_t *__restrict__ list,
             const uint32_t *__restrict__ offsets, uint32_t nb, int CH, uint32_t W, uint32_t B,
             uint32_t *__restrict__ buckets, uint32_t *__restrict__ ikeys, uint32_t *__restrict__ ivals,
-            uint32_t nslots) {
+            uint32_t nslots, const uint8_t *__restrict__ filled) {
   using F = typename C::Fp;
   constexpr int AW = aff_words<F>();  // u32 per internal-form point (multiple of 8)
   constexpr int NCH = AW / 4;         // 16-B chunks per point
   __shared__ uint4 stage[4][NCH][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  // this launch's list range [offsets[0], offsets[nb]) (one split of a split pipeline)
   const uint32_t total = offsets[nb];
-  const uint32_t cs = t * (uint32_t)CH;
+  const uint32_t cs = offsets[0] + t * (uint32_t)CH;
   const bool active = 2 * t < nslots && cs < total;
   uint32_t k0 = nb, k1 = nb;  // item keys of slots 2t, 2t+1
   uint32_t tail_b = nb, tail_slot = 0;  // the chunk's right-partial last run (began in the chunk), in acc
@@ -373,10 +377,18 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
       P.y.v[i] = w[F::SN + i];
     }
   };
+  // a run that starts in this chunk begins from the bucket's sum over the earlier splits
+  // (filled), else from infinity; a run continuing from an earlier chunk starts empty (its
+  // owner carries the earlier value)
+  auto start_run = [&](uint32_t b) {
+    if (filled && filled[b]) xyzz_load(acc, buckets + (size_t)b * xyzz_words<F>());
+    else xyzz_set_inf(acc);
+  };
   if (active) {
     const uint32_t ce = min(total, cs + (uint32_t)CH);
     uint32_t b = bucket_of(offsets, nb, cs);
     uint32_t bbeg = offsets[b], bend = offsets[b + 1];
+    if (bbeg >= cs) start_run(b);
     uint32_t bnext = offsets[min(b + 2, nb)];  // end of the next bucket, loaded ahead
     bool first_run = true;
     // Flushes store the accumulator LAZILY (X < 14p for the 381-bit madd): every
@@ -403,13 +415,13 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
           xyzz_store(buckets + (size_t)b * xyzz_words<F>(), acc);
         }
         first_run = false;
-        xyzz_set_inf(acc);
         do {  // next non-empty bucket; the next boundary is already in a register
           b++;
           bbeg = bend;
           bend = bnext;
           bnext = offsets[min(b + 2, nb)];
         } while (bend <= e);
+        start_run(b);
       }
       if (P.x.v[0] != 0xffffffffu) {  // affine infinity is skipped
         if (c0 & 0x80000000u) {
@@ -472,6 +484,15 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
     ikeys[2 * t] = k0;
     ikeys[2 * t + 1] = k1;
   }
+}
+
+// split pipelines: filled[b] = bucket b holds a sum (some split so far had entries for it)
+static __global__ void __launch_bounds__(256) k_fill_mark(const uint32_t *__restrict__ off, uint32_t nb, int first,
+                                                          uint8_t *__restrict__ filled) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint8_t f = off[b + 1] > off[b] ? 1 : 0;
+  filled[b] = first ? f : (uint8_t)(filled[b] | f);
 }
 
 // 5a. compaction of the partial items (keys < nb), order preserving: scatter by a
@@ -609,7 +630,8 @@ struct SegRegion {
 //    else Y1_(y - 2^l0).
 template <class C>
 __global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ buckets,
-                                              const uint32_t *__restrict__ offsets, int W, int c, int l0,
+                                              const uint32_t *__restrict__ offsets,
+                                              const uint8_t *__restrict__ filled, int W, int c, int l0,
                                               SegRegion r0, SegRegion r1, int wlanes,
                                               uint32_t *__restrict__ Y) {
   using F = typename C::Fp;
@@ -633,7 +655,7 @@ __global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ bucke
       const int s = lane * per + k;
       const uint32_t m = hiY ? ((uint32_t)seg << l0) + s : ((uint32_t)s << l0) + seg;
       const uint32_t rank = (uint32_t)w * B + m;
-      if (offsets[rank + 1] > offsets[rank]) {  // empty buckets hold garbage (never written)
+      if (filled ? filled[rank] != 0 : offsets[rank + 1] > offsets[rank]) {  // empty buckets hold garbage
         Xyzz<F> bm;
         xyzz_load(bm, buckets + ((size_t)w * B + m) * xyzz_words<F>());
         xyzz_add(acc, bm);
@@ -657,7 +679,8 @@ __global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ bucke
 //     ahead: at one or two waves per SIMD nothing else hides those latencies.
 template <class C, bool PF>
 __global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buckets,
-                                               const uint32_t *__restrict__ offsets, int W, int c, int l0,
+                                               const uint32_t *__restrict__ offsets,
+                                               const uint8_t *__restrict__ filled, int W, int c, int l0,
                                                SegRegion r0, SegRegion r1, uint32_t *__restrict__ Y) {
   using F = typename C::Fp;
   constexpr int XW = xyzz_words<F>();
@@ -682,21 +705,21 @@ __global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buck
   };
   Xyzz<F> acc;
   xyzz_set_inf(acc);
+  auto nonempty = [&](uint32_t rank) -> bool {  // empty buckets hold garbage (never written)
+    return filled ? filled[rank] != 0 : offsets[rank + 1] > offsets[rank];
+  };
   uint32_t m = bucket_m(part * per);
-  uint32_t rank = (uint32_t)w * B + m;
-  uint32_t o0 = offsets[rank], o1 = offsets[rank + 1];
+  bool nfull = nonempty((uint32_t)w * B + m);
   Xyzz<F> nxt;
   if (PF) xyzz_load(nxt, wb + (size_t)m * XW);
   for (int k = 0; k < per; k++) {
-    const bool full = o1 > o0;  // empty buckets hold garbage (never written)
+    const bool full = nfull;
     const uint32_t mc = m;
     Xyzz<F> cur;
     if (PF) cur = nxt;
     if (k + 1 < per) {
       m = bucket_m(part * per + k + 1);
-      rank = (uint32_t)w * B + m;
-      o0 = offsets[rank];
-      o1 = offsets[rank + 1];
+      nfull = nonempty((uint32_t)w * B + m);
       if (PF) xyzz_load(nxt, wb + (size_t)m * XW);
     }
     if (full) {
@@ -885,7 +908,12 @@ struct MsmShape {
   // two-level bucket sort: 2^fs fine buckets per coarse bin, nbins coarse bins per window,
   // level-1 workgroups of M entries (nwg per window)
   int fs, nbins, M, nwg;
-  size_t nmat() const { return (size_t)W * nbins * nwg; }
+  // point splits: the entries are sorted by (split, window, bucket), split h holding the pairs
+  // [n h / NS, n (h+1) / NS); each split is accumulated by its own launch (host-input calls
+  // start on the first split while the later splits' points still cross PCIe)
+  int NS;
+  size_t nmat() const { return (size_t)NS * W * nbins * nwg; }
+  int nsplit_max() const { return (n + NS - 1) / NS; }  // points of the largest split
 };
 
 static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; return r; }
@@ -894,11 +922,24 @@ static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; retu
 // MI355X (profiles/r01_*, profiles/r02h_qy_qa_sweep.txt): Y sums take 16 buckets per lane at
 // scale (8: ysum 0.37 -> 0.48 ms, 4: 0.66 ms at BLS12-381 2^20), the accumulation 64 sorted entries per lane (128 from 2^25
 // entries on, profiles/r01_v7_ch_sweep.txt).
-static MsmShape make_shape(int n, int c, int W) {
+#ifndef ZK_MSM_SPLITS
+#define ZK_MSM_SPLITS 2  // point splits of a host-input MSM pipeline (copy / accumulation overlap)
+#endif
+#ifndef ZK_MSM_SPLIT_MIN
+#define ZK_MSM_SPLIT_MIN (1 << 16)  // smallest host-input MSM that is split
+#endif
+#ifndef ZK_YSUM_LANES
+#define ZK_YSUM_LANES 65536  // Y-sum lanes at most (one wave per SIMD of 256 CUs)
+#endif
+#ifndef ZK_YSUM_PF
+#define ZK_YSUM_PF 1  // k_ysum2 loads the next bucket one iteration ahead
+#endif
+static MsmShape make_shape(int n, int c, int W, int NS = 1) {
   MsmShape s;
   s.n = n;
   s.c = c;
   s.W = W;
+  s.NS = NS;
   s.B = 1 << (c - 1);
   s.l0 = c / 2;  // l0 + l1 = c - 1, l0 >= l1
   s.l1 = c - 1 - s.l0;
@@ -910,7 +951,7 @@ static MsmShape make_shape(int n, int c, int W) {
   // 2^16: ysum 0.21 -> ~0.15 ms with QY 2 -> 4, profiles/r02y_msm_small_ab.txt)
   {
     const size_t adds = 2 * (size_t)s.W * (size_t)s.B;
-    int q = (int)((adds + 65535) >> 16);  // rounded up: at most ~64K lanes, one wave per SIMD
+    int q = (int)((adds + ZK_YSUM_LANES - 1) / ZK_YSUM_LANES);  // rounded up: at most ZK_YSUM_LANES lanes
     q = q < 1 ? 1 : (q > 16 ? 16 : q);
     s.QY = pow2(q) < q ? 2 * pow2(q) : pow2(q);  }
   auto clampG = [](int g) { return g < 1 ? 1 : (g > 64 ? 64 : g); };
@@ -926,7 +967,7 @@ static MsmShape make_shape(int n, int c, int W) {
     size_t M = ((size_t)W * n + 2047) / 2048;
     M = (M + 255) & ~(size_t)255;
     s.M = (int)(M < 2048 ? 2048 : M);
-    s.nwg = (int)(((size_t)n + s.M - 1) / s.M);
+    s.nwg = (int)(((size_t)s.nsplit_max() + s.M - 1) / s.M);
   }
   // entries per thread in the level-0 accumulation: 64 at scale (~2^17+ lanes), fewer for
   // small inputs so the serial chain per lane stays short (a lone lane's madd ~12 us)
@@ -944,7 +985,7 @@ static MsmShape make_shape(int n, int c, int W) {
 template <class F>
 constexpr int stitch_bs() { return xyzz_words<F>() > 64 ? 128 : 256; }
 
-static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.n + s.CH - 1) / s.CH); }
+static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.nsplit_max() + s.CH - 1) / s.CH); }
 static size_t stitch_slots1(const MsmShape &s, int bs) { return 2 * ((stitch_slots0(s) + bs - 1) / bs) + 2; }
 
 // sorted entries of one pipeline pass: passes of several windows are kept at <= 2^30 entries
@@ -977,7 +1018,8 @@ static size_t group_bytes(const MsmShape &s) {
   add(maxent * 4 * 3);                    // digits, level-1 values, list
   add(maxent * 2);                        // level-1 fine indices
   add((s.nmat() + 1) * 4 * 2);            // level-1 counts, their scan
-  add((nb + 1) * 4);                      // offsets
+  add((s.NS * nb + 1) * 4);               // offsets (every split)
+  add(nb);                                // filled flags (split pipelines)
   add(ns0 * (xw + 4) + ns0 * 16 + 64);    // level-0 items, compacted keys + index, flags, pos, count
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
@@ -1062,6 +1104,10 @@ struct GroupPass {
   uint32_t *okA, *ovA, *okB, *ovB, *buckets, *Y;
   uint64_t *exp;
   void *cubtmp;
+  uint8_t *filled = nullptr;  // split pipelines: bucket b holds a sum from an earlier split
+  // split pipelines: split h's accumulation waits for wait_split[h] (its points converted on the
+  // aux stream); empty: the points are resident
+  std::vector<hipEvent_t> wait_split;
   // stitch state (level ping-pong)
   const uint32_t *inK, *inV;
   size_t slots;
@@ -1082,7 +1128,8 @@ struct GroupPass {
     tmpf = dev.arena.take<uint16_t>(maxent);  // level-1 order: fine bucket within the coarse bin
     cnt = dev.arena.take<uint32_t>(s.nmat() + 1);
     coff = dev.arena.take<uint32_t>(s.nmat() + 1);
-    offsets = dev.arena.take<uint32_t>(nb + 1);
+    offsets = dev.arena.take<uint32_t>((size_t)s.NS * nb + 1);
+    if (s.NS > 1) filled = dev.arena.take<uint8_t>(nb);
     ns0 = stitch_slots0(s);
     ns1 = stitch_slots1(s, STITCH_BS);
     ikeys0 = dev.arena.take<uint32_t>(ns0);
@@ -1115,34 +1162,68 @@ struct GroupPass {
                        sc.mont ? 1 : 0, c, wbase, s.W, dig);
     ZK_CHECK(hipGetLastError());
     mark("digits");
-    const dim3 grid((unsigned)s.nwg, (unsigned)s.W);
-    hipLaunchKernelGGL(k_coarse<false>, grid, dim3(256), 0, st, dig, n, s.M, s.fs, s.nbins, cnt, tmpv, tmpf);
+    const dim3 grid((unsigned)s.nwg, (unsigned)(s.W * s.NS));  // virtual windows: (split, window)
+    hipLaunchKernelGGL(k_coarse<false>, grid, dim3(256), 0, st, dig, n, s.M, s.fs, s.nbins, s.W, s.NS, cnt, tmpv,
+                       tmpf);
     ZK_CHECK(hipGetLastError());
     size_t cb = cub;
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, cnt, coff, (int)(s.nmat() + 1), st));
-    hipLaunchKernelGGL(k_coarse<true>, grid, dim3(256), 0, st, dig, n, s.M, s.fs, s.nbins, coff, tmpv, tmpf);
+    hipLaunchKernelGGL(k_coarse<true>, grid, dim3(256), 0, st, dig, n, s.M, s.fs, s.nbins, s.W, s.NS, coff, tmpv,
+                       tmpf);
     ZK_CHECK(hipGetLastError());
     const int cap = fine_stage_cap(s.fs);
     const int lds = (4 << s.fs) + 4 * cap;
     ZK_CHECK(hipFuncSetAttribute((const void *)k_fine, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    const uint32_t nq = (uint32_t)(s.W * s.nbins);
+    const uint32_t nq = (uint32_t)(s.NS * s.W * s.nbins);
     hipLaunchKernelGGL(k_fine, dim3(nq), dim3(256), lds, st, coff, s.nwg, nq, s.fs, cap, tmpv, tmpf, list, offsets);
     ZK_CHECK(hipGetLastError());
     mark("sort");
   }
 
-  void accumulate() {
-    timer_begin(dev, timer_slot, st);
-    // upper bound on the chunk count; threads past offsets[nb] only clear their item slots
-    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(ns0 / 2, 256)), dim3(256), 0, st, pts_int, list, offsets,
-                       (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0, ivals0, (uint32_t)ns0);
+  // accumulation of split sp: list range [offsets[sp nb], offsets[(sp+1) nb]); a run that starts
+  // in a lane's chunk begins from the earlier splits' bucket sum (filled)
+  const std::atomic<int> *split_ready = nullptr;  // set by the copy thread once wait_split[h] is recorded
+  void accumulate(int sp) {
+    if (sp < (int)wait_split.size() && wait_split[sp]) {
+      // the event must be recorded (host order) before this stream waits on it
+      if (split_ready)
+        while (!split_ready[sp].load(std::memory_order_acquire)) std::this_thread::yield();
+      ZK_CHECK(hipStreamWaitEvent(st, wait_split[sp], 0));
+    }
+    if (sp == 0) timer_begin(dev, timer_slot, st);
+    const size_t npts = (size_t)s.n * (sp + 1) / s.NS - (size_t)s.n * sp / s.NS;
+    const size_t nsl = 2 * (((size_t)s.W * npts + s.CH - 1) / s.CH);  // <= ns0
+    // upper bound on the chunk count; threads past the range's end only clear their item slots
+    hipLaunchKernelGGL(k_accum<C>, dim3(div_up(nsl / 2, 256)), dim3(256), 0, st, pts_int, list,
+                       offsets + (size_t)sp * nb, (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0,
+                       ivals0, (uint32_t)nsl, (const uint8_t *)(sp > 0 ? filled : nullptr));
     ZK_CHECK(hipGetLastError());
-    timer_end(dev, timer_slot, st);
+    if (sp == s.NS - 1) timer_end(dev, timer_slot, st);
     mark("accum");
     inK = ikeys0;
     inV = ivals0;
-    slots = ns0;
+    slots = nsl;
     outK = okA; outV = ovA; altK = okB; altV = ovB;
+  }
+  // split pipelines: every bucket of the split complete before the next split starts from them
+  void complete_stitch() {
+    if (done) return;
+    ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
+    stream_wait(dev, st);
+    if (*hc > (uint32_t)STITCH_BS) {
+      for (;;) {
+        if (stitch_level()) break;
+        ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
+        ZK_CHECK(hipStreamSynchronize(st));
+        if (*hc <= (uint32_t)STITCH_BS) break;
+      }
+    }
+    done = true;
+  }
+  void fill_mark(int sp) {
+    hipLaunchKernelGGL(k_fill_mark, dim3(div_up(nb, 256)), dim3(256), 0, st, offsets + (size_t)sp * nb, (uint32_t)nb,
+                       sp == 0 ? 1 : 0, filled);
+    ZK_CHECK(hipGetLastError());
   }
 
   // stitch level: compact the partial items, sum them per bucket (k_stitch_blk); true when
@@ -1173,12 +1254,12 @@ struct GroupPass {
     const int n0 = s.r0.count * s.r0.G, n1 = s.r1.count * s.r1.G;
     if (n0 % 256 == 0 && n1 % 256 == 0) {  // block-level Y sums (every shape from c = 12 up)
       const unsigned nblk = (unsigned)(s.W * (n0 + n1) / 256);
-      hipLaunchKernelGGL((k_ysum2<C, true>), dim3(nblk), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0, s.r1,
-                         Y);
+      hipLaunchKernelGGL((k_ysum2<C, ZK_YSUM_PF != 0>), dim3(nblk), dim3(256), 0, st, buckets, offsets,
+                         (const uint8_t *)filled, s.W, c, s.l0, s.r0, s.r1, Y);
     } else {  // small shapes: in-wavefront segments
       const size_t lanes = (size_t)s.W * s.ylanes;
-      hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets, s.W, c, s.l0, s.r0,
-                         s.r1, s.ylanes, Y);
+      hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets,
+                         (const uint8_t *)filled, s.W, c, s.l0, s.r0, s.r1, s.ylanes, Y);
     }
     ZK_CHECK(hipGetLastError());
     mark("ysum");
@@ -1194,8 +1275,15 @@ struct GroupPass {
   static constexpr int SPECULATIVE_LEVELS = 3;
   void launch() {
     sort();
-    accumulate();
-    for (int lv = 0; lv < SPECULATIVE_LEVELS && !done; lv++) done = stitch_level();
+    for (int sp = 0; sp < s.NS; sp++) {
+      accumulate(sp);
+      done = false;
+      for (int lv = 0; lv < SPECULATIVE_LEVELS && !done; lv++) done = stitch_level();
+      if (s.NS > 1) {
+        if (sp < s.NS - 1) complete_stitch();
+        fill_mark(sp);
+      }
+    }
     mark("stitch");
     if (!done) ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
     reduce_tail();
@@ -1299,7 +1387,10 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   // halve the windows per pass (the result does not depend on the grouping) down to one window
   // before giving up -- instead of aborting the caller's process on the first failed hipMalloc.
   bool dropped_twiddles = false;
-  MsmShape s = make_shape(n, c, Wg);
+  // Host inputs in one pipeline pass: the points are split ZK_MSM_SPLITS ways, split h is
+  // accumulated as soon as its points have landed while the next split's cross PCIe
+  auto splits = [&](int wg) { return (host_inputs && wg == W && n >= ZK_MSM_SPLIT_MIN) ? ZK_MSM_SPLITS : 1; };
+  MsmShape s = make_shape(n, c, Wg, splits(Wg));
   while (!dev.arena.try_reserve(sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(s))) {
     if (!dropped_twiddles) {
       ZK_CHECK(hipStreamSynchronize(st));
@@ -1309,27 +1400,58 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
     }
     ZK_REQUIRE(Wg > 1, "msm: out of device memory (one window per pass does not fit)");
     Wg = (Wg + 1) / 2;
-    s = make_shape(n, c, Wg);
+    s = make_shape(n, c, Wg, splits(Wg));
   }
+  const int NS = s.NS;
   msm_last_groups().store((W + Wg - 1) / Wg);
   dev.arena.reset();
   ScalarSlice sc = sc_in;
-  const uint64_t *d_pt = points;
+  uint32_t *pts_int = nullptr;
+  PhaseProf prof(st);
+  bool points_on_aux = false;
+  std::thread copier;
+  std::atomic<int> split_ready[ZK_MSM_SPLITS];
   if (host_inputs) {
     uint64_t *a = dev.arena.take<uint64_t>((size_t)n * sc_in.stride);
     uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
-    // caller memory is pageable; the runtime's pageable path runs at PCIe rate on MI355X
-    // hosts (56 GB/s measured, tools/microbench/copy_bw.hip), a pinned bounce buffer only
-    // adds a host copy
+    pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
+    // Caller memory is pageable; the runtime's pageable path runs at PCIe rate on MI355X hosts
+    // (56 GB/s measured, tools/microbench/copy_bw.hip), a pinned bounce buffer only adds a host
+    // copy.  The scalars go first on the main stream (the digits and the bucket sort need only
+    // them); the points follow on the context's second stream in chunks, each converted to the
+    // internal form as soon as it lands, and the accumulation waits for the last chunk -- so
+    // the sort runs while the 96 B/pair of points are still crossing PCIe.
     ZK_CHECK(hipMemcpyAsync(a, sc_in.data, sc_bytes, hipMemcpyHostToDevice, st));
-    ZK_CHECK(hipMemcpyAsync(b, points, pt_bytes, hipMemcpyHostToDevice, st));
     sc.data = a;
-    d_pt = b;
+    // A copy from pageable memory returns only once it is staged, so the points are issued by a
+    // thread of their own: the calling thread goes on to enqueue the sort (and split 0's
+    // accumulation as soon as split 0's points are recorded) while the copies proceed.
+    hipStream_t st2 = dev.aux_stream();
+    for (int h = 0; h < NS; h++) dev.split_event(h);  // created here, before the thread uses them
+    for (int h = 0; h < NS; h++) split_ready[h].store(0, std::memory_order_relaxed);
+    copier = std::thread([&dev, st2, NS, n, b, points, pts_int, &split_ready] {
+      ZK_CHECK(hipSetDevice(dev.id));
+      const int chunk = 1 << 17;  // points per copy chunk (12 MiB of BLS12-381 points)
+      for (int h = 0; h < NS; h++) {
+        const int lo = (int)((int64_t)n * h / NS), hi = (int)((int64_t)n * (h + 1) / NS);
+        for (int p0 = lo; p0 < hi; p0 += chunk) {
+          const int cnt = std::min(chunk, hi - p0);
+          const size_t off = (size_t)p0 * 2 * C::NP64;
+          ZK_CHECK(hipMemcpyAsync(b + off, points + off, (size_t)cnt * 2 * C::NP64 * 8, hipMemcpyHostToDevice, st2));
+          hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(cnt, 256)), dim3(256), 0, st2, b + off, cnt,
+                             pts_int + (size_t)p0 * aff_words<F>());
+          ZK_CHECK(hipGetLastError());
+        }
+        ZK_CHECK(hipEventRecord(dev.split_event(h), st2));
+        split_ready[h].store(1, std::memory_order_release);
+      }
+    });
+    points_on_aux = true;
+  } else {
+    pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
+    hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, points, n, pts_int);
+    ZK_CHECK(hipGetLastError());
   }
-  uint32_t *pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
-  PhaseProf prof(st);
-  hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, d_pt, n, pts_int);
-  ZK_CHECK(hipGetLastError());
   prof.mark("points");
   const size_t mark = dev.arena.used();
   const size_t per_w = (size_t)c * 4 * C::NP64;  // exported u64 per window
@@ -1343,9 +1465,21 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
     dev.arena.rewind(mark);
     const MsmShape sg = (wbase + Wg <= W) ? s : make_shape(n, c, W - wbase);
     GroupPass<C> pass(dev, sg, sc, wbase, pts_int, h + (size_t)wbase * per_w, hc, &prof, st, wbase == 0 ? 0 : -1);
+    if (points_on_aux) {  // joined once: later groups follow on the same stream
+      if (sg.NS == NS) {
+        for (int h = 0; h < NS; h++) pass.wait_split.push_back(dev.split_event(h));
+        pass.split_ready = split_ready;
+      } else {  // (one split pipeline per call: only a single-pass shape is split)
+        if (copier.joinable()) copier.join();
+        pass.wait_split.assign(1, dev.split_event(NS - 1));
+      }
+    }
+    points_on_aux = false;
     pass.launch();
+    if (copier.joinable()) copier.join();  // every copy is issued (the stream order does the rest)
     pass.finish();
   }
+  if (copier.joinable()) copier.join();
   timer_collect(dev);
   const auto t0 = std::chrono::steady_clock::now();
   finish_host<C>(c, W, h, out);
@@ -1369,7 +1503,8 @@ size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int windo
   const size_t sc_bytes = host_inputs ? (size_t)n * nl * 8 : 0;
   const size_t pt_bytes = host_inputs ? (size_t)n * 2 * C::NP64 * 8 : 0;
   const size_t int_bytes = (size_t)n * aff_words<F>() * 4;
-  return sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(make_shape(n, c, Wg));
+  const int NS = (host_inputs && Wg == W && n >= ZK_MSM_SPLIT_MIN) ? ZK_MSM_SPLITS : 1;
+  return sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(make_shape(n, c, Wg, NS));
 }
 
 // One complete MSM on one device context (caller holds dev.mu): every scalar slice.

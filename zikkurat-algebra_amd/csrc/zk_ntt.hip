@@ -17,8 +17,11 @@
 // output straight to its natural index k = sum_q k_q T_q (no bit-reversal pass).
 // Inverse: w -> w^-1 and the 1/N factor folded into pass 0's twiddle table.
 // Twiddle tables are built on the device once per (curve, m, gen, direction) and cached.
+#include <sys/mman.h>
+#include <algorithm>
 #include <atomic>
 #include <map>
+#include <thread>
 #include <tuple>
 #include <vector>
 #include "zk_field.hpp"
@@ -598,12 +601,117 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
   return g_tw.emplace(key, ts).first->second;
 }
 
+// The caller's output array is often freshly allocated (the Haskell binding allocates a new
+// FlatArray per call, Poly.hs:405,417): its first touch (page faults, ~13 GB/s) would otherwise
+// happen inside the device-to-host copy.  The pages are populated for writing -- contents
+// untouched, so in-place calls are safe -- by host threads while the input copy and the passes
+// run.  (MADV_POPULATE_WRITE, Linux >= 5.14; on older kernels the call fails and nothing changes.)
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+static void prefault_for_write(void *p, size_t bytes, std::vector<std::thread> &threads) {
+  if (bytes < ((size_t)4 << 20)) return;
+  const size_t page = 4096;
+  const uintptr_t lo = (uintptr_t)p & ~(uintptr_t)(page - 1);
+  const uintptr_t hi = ((uintptr_t)p + bytes + page - 1) & ~(uintptr_t)(page - 1);
+  const size_t span = hi - lo;
+  const int nt = span >= ((size_t)64 << 20) ? 8 : 1;
+  const size_t part = ((span / nt) + page - 1) & ~(page - 1);
+  for (int k = 0; k < nt; k++) {
+    const uintptr_t a = lo + k * part;
+    if (a >= hi) break;
+    const size_t len = std::min<size_t>(part, hi - a);
+    threads.emplace_back([a, len] { (void)madvise((void *)a, len, MADV_POPULATE_WRITE); });
+  }
+}
+
 struct CfgBN { using Fd = BN_Fr; using Fh = zkh::BN_Fr; };
 struct CfgBLS { using Fd = BLS_Fr; using Fh = zkh::BLS_Fr; };
 
+// Host I/O spread over a device set (zkg_set_devices): the transform runs on the first listed
+// device; chunk k of the input / output crosses PCIe through listed device k (its own link) and
+// moves between device k and the compute device over xGMI (peer copies; a plain device-to-device
+// copy when both are the same GPU).  One host thread per helper drives its copies, so the links
+// run concurrently.
+struct Spread {
+  std::vector<Device *> helpers;  // listed devices 1 .. G-1 (contexts, locked by the caller)
+  int G = 1;
+};
+
+static void enable_peer(int a, int b) {
+  if (a == b) return;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) {
+    (void)hipGetLastError();
+    return;
+  }
+  int prev = 0;
+  ZK_CHECK(hipGetDevice(&prev));
+  ZK_CHECK(hipSetDevice(a));
+  const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+  if (e != hipSuccess) (void)hipGetLastError();  // already enabled
+  ZK_CHECK(hipSetDevice(prev));
+}
+
+// chunk k of n bytes (k = 0 .. G-1), 4 KiB aligned boundaries
+static void spread_chunk(size_t n, int G, int k, size_t &off, size_t &len) {
+  const size_t a = (n / G * k) & ~(size_t)4095, b = k + 1 == G ? n : ((n / G * (k + 1)) & ~(size_t)4095);
+  off = a;
+  len = b - a;
+}
+
+// host -> device-0 buffer `d` (bytes), chunk 0 by dev0's own stream (caller's thread)
+static void spread_in(Device &dev0, const Spread &sp, uint64_t *d, const uint64_t *h, size_t bytes) {
+  std::vector<std::thread> th;
+  for (int k = 1; k < sp.G; k++) {
+    th.emplace_back([&, k] {
+      Device &hk = *sp.helpers[k - 1];
+      size_t off, len;
+      spread_chunk(bytes, sp.G, k, off, len);
+      if (!len) return;
+      ZK_CHECK(hipSetDevice(hk.id));
+      uint64_t *buf = hk.arena.take<uint64_t>(len / 8);
+      ZK_CHECK(hipMemcpyAsync(buf, (const char *)h + off, len, hipMemcpyHostToDevice, hk.stream));
+      if (hk.id == dev0.id) ZK_CHECK(hipMemcpyAsync((char *)d + off, buf, len, hipMemcpyDeviceToDevice, hk.stream));
+      else ZK_CHECK(hipMemcpyPeerAsync((char *)d + off, dev0.id, buf, hk.id, len, hk.stream));
+      ZK_CHECK(hipStreamSynchronize(hk.stream));
+    });
+  }
+  size_t off, len;
+  spread_chunk(bytes, sp.G, 0, off, len);
+  ZK_CHECK(hipMemcpyAsync((char *)d + off, (const char *)h + off, len, hipMemcpyHostToDevice, dev0.stream));
+  for (auto &t : th) t.join();
+  ZK_CHECK(hipSetDevice(dev0.id));
+}
+
+// device-0 buffer `d` -> host (dev0's stream is idle: the passes have completed)
+static void spread_out(Device &dev0, const Spread &sp, uint64_t *h, const uint64_t *d, size_t bytes) {
+  std::vector<std::thread> th;
+  for (int k = 1; k < sp.G; k++) {
+    th.emplace_back([&, k] {
+      Device &hk = *sp.helpers[k - 1];
+      size_t off, len;
+      spread_chunk(bytes, sp.G, k, off, len);
+      if (!len) return;
+      ZK_CHECK(hipSetDevice(hk.id));
+      hk.arena.reset();
+      uint64_t *buf = hk.arena.take<uint64_t>(len / 8);
+      if (hk.id == dev0.id) ZK_CHECK(hipMemcpyAsync(buf, (const char *)d + off, len, hipMemcpyDeviceToDevice, hk.stream));
+      else ZK_CHECK(hipMemcpyPeerAsync(buf, hk.id, (const char *)d + off, dev0.id, len, hk.stream));
+      ZK_CHECK(hipMemcpyAsync((char *)h + off, buf, len, hipMemcpyDeviceToHost, hk.stream));
+      ZK_CHECK(hipStreamSynchronize(hk.stream));
+    });
+  }
+  size_t off, len;
+  spread_chunk(bytes, sp.G, 0, off, len);
+  ZK_CHECK(hipMemcpyAsync((char *)h + off, (const char *)d + off, len, hipMemcpyDeviceToHost, dev0.stream));
+  for (auto &t : th) t.join();
+  ZK_CHECK(hipSetDevice(dev0.id));
+}
+
 template <class Cfg>
 static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst,
-                    bool host_io, bool inverse) {
+                    bool host_io, bool inverse, const Spread *sp = nullptr) {
   using F = typename Cfg::Fd;
   const size_t N = (size_t)1 << m;
   hipStream_t st = dev.stream;
@@ -633,11 +741,28 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   dev.arena.reset();
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
+  std::vector<std::thread> prefault;
   if (host_io) {
     uint64_t *a = dev.arena.take<uint64_t>(N * F::N64);
-    ZK_CHECK(hipMemcpyAsync(a, src, N * elbytes, hipMemcpyHostToDevice, st));
     d_src = a;
     d_dst = dev.arena.take<uint64_t>(N * F::N64);
+    prefault_for_write(dst, N * elbytes, prefault);
+    if (sp) {
+      for (Device *hk : sp->helpers) {  // chunk staging on every helper
+        size_t off, len, mx = 0;
+        for (int k = 0; k < sp->G; k++) {
+          spread_chunk(N * elbytes, sp->G, k, off, len);
+          mx = std::max(mx, len);
+        }
+        ZK_CHECK(hipSetDevice(hk->id));
+        hk->arena.reserve(mx + 4096);
+        hk->arena.reset();
+      }
+      ZK_CHECK(hipSetDevice(dev.id));
+      spread_in(dev, *sp, a, src, N * elbytes);
+    } else {
+      ZK_CHECK(hipMemcpyAsync(a, src, N * elbytes, hipMemcpyHostToDevice, st));
+    }
   }
   uint64_t *scratch = dev.arena.take<uint64_t>(N * F::N64);
 
@@ -688,7 +813,15 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     in = out;
     T <<= r;
   }
-  if (host_io) ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
+  if (host_io) {
+    for (auto &t : prefault) t.join();
+    if (sp) {
+      stream_wait(dev, st);
+      spread_out(dev, *sp, dst, d_dst, N * elbytes);
+    } else {
+      ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
+    }
+  }
   stream_wait(dev, st);
   timer_collect(dev);
 }
@@ -708,6 +841,36 @@ void ntt_release(Device &dev) {
 void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst, bool host_io,
          bool inverse) {
   ZK_REQUIRE(m >= 0 && m <= 30, "ntt: log2 size out of range (0..30)");
+  const std::vector<int> set = host_io && m >= 16 ? device_set() : std::vector<int>();
+  if (set.size() > 1) {
+    // compute on the first listed device, host I/O spread over every listed one; the contexts
+    // are locked in uid order (concurrent calls with other sets cannot deadlock)
+    const int G = (int)set.size();
+    std::vector<Device *> ctx(G);
+    for (int k = 0; k < G; k++) {
+      int slot = 0;
+      for (int j = 0; j < k; j++) slot += set[j] == set[k];
+      ctx[k] = &device_context(set[k], slot);
+    }
+    std::vector<Device *> order = ctx;
+    std::sort(order.begin(), order.end(), [](Device *a, Device *b) { return a->uid < b->uid; });
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (Device *d : order) locks.emplace_back(d->mu);
+    Spread sp;
+    sp.G = G;
+    sp.helpers.assign(ctx.begin() + 1, ctx.end());
+    for (int k = 1; k < G; k++) {
+      enable_peer(set[0], set[k]);
+      enable_peer(set[k], set[0]);
+    }
+    int prev = 0;
+    ZK_CHECK(hipGetDevice(&prev));
+    ZK_CHECK(hipSetDevice(set[0]));
+    if (curve == 0) ntt_run<CfgBN>(*ctx[0], curve, m, gen_mont, src, dst, host_io, inverse, &sp);
+    else ntt_run<CfgBLS>(*ctx[0], curve, m, gen_mont, src, dst, host_io, inverse, &sp);
+    ZK_CHECK(hipSetDevice(prev));
+    return;
+  }
   Device &dev = current_device();
   std::lock_guard<std::mutex> lock(dev.mu);
   if (curve == 0) ntt_run<CfgBN>(dev, curve, m, gen_mont, src, dst, host_io, inverse);

@@ -65,6 +65,23 @@ void *Device::host_staging(size_t bytes) {
   return pinned;
 }
 
+hipStream_t Device::aux_stream() {
+  if (!aux) {
+    ZK_CHECK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    ZK_CHECK(hipEventCreateWithFlags(&aux_ev, hipEventDisableTiming));
+  }
+  return aux;
+}
+
+hipEvent_t Device::split_event(int h) {
+  while ((int)split_ev.size() <= h) {
+    hipEvent_t e;
+    ZK_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    split_ev.push_back(e);
+  }
+  return split_ev[h];
+}
+
 void Device::release_memory() {
   arena.release();
   if (pinned) ZK_CHECK(hipHostFree(pinned));

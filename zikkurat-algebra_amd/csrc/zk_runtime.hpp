@@ -92,6 +92,13 @@ struct Device {
   void *host_staging(size_t bytes);
   KernelTimer timer;
   hipEvent_t sync_ev = nullptr;  // stream_wait's marker
+  // second stream of this context (host-input copies overlapping the first stream's work) and
+  // an event to join it; created on first use (aux_stream)
+  hipStream_t aux = nullptr;
+  hipEvent_t aux_ev = nullptr;
+  hipStream_t aux_stream();
+  std::vector<hipEvent_t> split_ev;  // per point split of a host-input MSM (split_event)
+  hipEvent_t split_event(int h);
   void release_memory();         // arena + pinned staging (caller holds mu, stream idle)
 };
 

@@ -138,11 +138,11 @@ struct DigitStream {
 //    inside a bucket depends on atomic timing; bucket sums are group sums, so the
 //    canonical result does not.
 template <class C>
-__global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int stride, int loff,
-                                                int nread, int mont, int c, int wbase, int Wg,
+__global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ scalars, int n, int plo, int phi,
+                                                int stride, int loff, int nread, int mont, int c, int wbase, int Wg,
                                                 uint32_t *__restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const int i = plo + blockIdx.x * blockDim.x + threadIdx.x;  // points [plo, phi) of n
+  if (i >= phi) return;
   DigitStream<C> ds;
   ds.load(scalars, i, stride, loff, nread, mont);
   for (int w = 0; w < wbase + Wg; w++) {
@@ -185,19 +185,17 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *tmp
 // matrix gives this workgroup's first slot in every bin; entries go through LDS in chunks,
 // sorted by bin there, so every bin's run leaves as consecutive lanes' stores.
 template <bool SCATTER>
-__global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig, int n, int M, int s, int nbins,
-                                                int W, int NS, uint32_t *__restrict__ cnt,
+__global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig, int n, int plo, int phi, int M,
+                                                int s, int nbins, uint32_t *__restrict__ cnt,
                                                 uint32_t *__restrict__ tmpv, uint16_t *__restrict__ tmpf) {
   __shared__ uint32_t hist[MSM_COARSE_BINS], lofs[MSM_COARSE_BINS], gcur[MSM_COARSE_BINS], scan_tmp[256];
   __shared__ uint32_t sv[SORT_CHUNK], sk[SORT_CHUNK];
-  // virtual window wv = split * W + window: the split's points [n h / NS, n (h+1) / NS) of the window
-  const uint32_t wv = blockIdx.y, g = blockIdx.x, nwg = gridDim.x;
-  const uint32_t w = wv % (uint32_t)W, h = wv / (uint32_t)W;
+  // window w = blockIdx.y over the points [plo, phi) of one split (tmpv / tmpf: that split's region)
+  const uint32_t w = blockIdx.y, g = blockIdx.x, nwg = gridDim.x;
   const int t = threadIdx.x;
-  const int plo = (int)((int64_t)n * h / NS), phi = (int)((int64_t)n * (h + 1) / NS);
   const int e0 = plo + (int)g * M, e1 = min(phi, e0 + M);
   const uint32_t *d = dig + (size_t)w * n;
-  uint32_t *cw = cnt + (size_t)wv * nbins * nwg + g;
+  uint32_t *cw = cnt + (size_t)w * nbins * nwg + g;
   if (!SCATTER) {
     if (w == 0 && g == 0 && t == 0) cnt[(size_t)gridDim.y * nbins * nwg] = 0;  // the scan's total slot
     for (int b = t; b < nbins; b += 256) hist[b] = 0;
@@ -263,7 +261,9 @@ __global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig
 static __global__ void __launch_bounds__(256) k_fine(const uint32_t *__restrict__ coff, int nwg, uint32_t nq, int s,
                                                      int cap, const uint32_t *__restrict__ tmpv,
                                                      const uint16_t *__restrict__ tmpf, uint32_t *__restrict__ list,
-                                                     uint32_t *__restrict__ offsets) {
+                                                     uint32_t *__restrict__ offsets, uint32_t base) {
+  // tmpv / tmpf / list point at this split's region, which starts at list position `base`:
+  // the offsets written are absolute list positions
   extern __shared__ uint32_t fh[];
   __shared__ uint32_t part[256];
   const int F = 1 << s, t = threadIdx.x;
@@ -290,11 +290,11 @@ static __global__ void __launch_bounds__(256) k_fine(const uint32_t *__restrict_
     if (f < F) {
       const uint32_t h = fh[f];
       fh[f] = staged ? run : start + run;
-      offsets[(size_t)q * F + f] = start + run;
+      offsets[(size_t)q * F + f] = base + start + run;
       run += h;
     }
   }
-  if (q == nq - 1 && t == 0) offsets[(size_t)nq * F] = end;
+  if (q == nq - 1 && t == 0) offsets[(size_t)nq * F] = base + end;
   __syncthreads();
   if (staged) {
     for (uint32_t e = start + t; e < end; e += 256) sv[atomicAdd(&fh[tmpf[e]], 1u)] = tmpv[e];
@@ -912,7 +912,7 @@ struct MsmShape {
   // [n h / NS, n (h+1) / NS); each split is accumulated by its own launch (host-input calls
   // start on the first split while the later splits' points still cross PCIe)
   int NS;
-  size_t nmat() const { return (size_t)NS * W * nbins * nwg; }
+  size_t nmat() const { return (size_t)W * nbins * nwg; }  // level-1 count matrix of one split
   int nsplit_max() const { return (n + NS - 1) / NS; }  // points of the largest split
 };
 
@@ -923,11 +923,18 @@ static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; retu
 // scale (8: ysum 0.37 -> 0.48 ms, 4: 0.66 ms at BLS12-381 2^20), the accumulation 64 sorted entries per lane (128 from 2^25
 // entries on, profiles/r01_v7_ch_sweep.txt).
 #ifndef ZK_MSM_SPLITS
-#define ZK_MSM_SPLITS 2  // point splits of a host-input MSM pipeline (copy / accumulation overlap)
+#define ZK_MSM_SPLITS 4  // most splits of a host-input MSM pipeline (copy / sort / accumulation overlap)
 #endif
-#ifndef ZK_MSM_SPLIT_MIN
-#define ZK_MSM_SPLIT_MIN (1 << 16)  // smallest host-input MSM that is split
-#endif
+// Splits of a host-input MSM whose windows fit one pipeline pass: 4 from 2^19 pairs (splits of
+// >= 2^17 pairs keep every accumulation launch at >= 2 waves per SIMD), 2 from 2^17, else 1
+// (BLS12-381 2^20 through the reference symbol: 6.3-6.4 ms unsplit, 5.4-5.5 ms in two splits,
+// 4.8-4.9 ms in four, profiles/r03e_split_e2e.txt)
+static int msm_splits(int n, bool host_inputs, bool one_pass) {
+  if (!host_inputs || !one_pass) return 1;
+  if (n >= (1 << 19)) return ZK_MSM_SPLITS;
+  if (n >= (1 << 17)) return ZK_MSM_SPLITS < 2 ? ZK_MSM_SPLITS : 2;
+  return 1;
+}
 #ifndef ZK_YSUM_LANES
 #define ZK_YSUM_LANES 65536  // Y-sum lanes at most (one wave per SIMD of 256 CUs)
 #endif
@@ -972,7 +979,7 @@ static MsmShape make_shape(int n, int c, int W, int NS = 1) {
   // entries per thread in the level-0 accumulation: 64 at scale (~2^17+ lanes), fewer for
   // small inputs so the serial chain per lane stays short (a lone lane's madd ~12 us)
   {
-    const size_t ent = (size_t)s.W * (size_t)n;
+    const size_t ent = (size_t)s.W * (size_t)s.nsplit_max();  // entries of one accumulation launch
     size_t ch = ent >> 17;
     s.CH = ch >= 64 ? 64 : (ch <= 4 ? 4 : (int)ch);
     if (ent >= ((size_t)1 << 25)) s.CH = 128;
@@ -1018,7 +1025,7 @@ static size_t group_bytes(const MsmShape &s) {
   add(maxent * 4 * 3);                    // digits, level-1 values, list
   add(maxent * 2);                        // level-1 fine indices
   add((s.nmat() + 1) * 4 * 2);            // level-1 counts, their scan
-  add((s.NS * nb + 1) * 4);               // offsets (every split)
+  add(s.NS * (nb + 1) * 4);               // offsets (every split)
   add(nb);                                // filled flags (split pipelines)
   add(ns0 * (xw + 4) + ns0 * 16 + 64);    // level-0 items, compacted keys + index, flags, pos, count
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
@@ -1082,8 +1089,9 @@ struct ScalarSlice {
 // One pass of the device pipeline over windows [wbase, wbase + s.W): digits, bucket sort,
 // accumulation, stitch, Y sums, job sums, export; the (window, job) sums land in the pinned
 // host buffer h (reference-form XYZZ, window-major).  launch() enqueues everything on the
-// pass's stream without a host round trip; finish() synchronises it and, only for skewed
-// scalars whose partial runs need more than the speculative stitch levels, runs the rest.
+// pass's stream without a host round trip; finish() waits for it.  With NS point splits every
+// split is sorted into its own list region and accumulated on its own (split pipelines, for
+// host inputs that arrive split by split).
 template <class C>
 struct GroupPass {
   using F = typename C::Fp;
@@ -1094,29 +1102,23 @@ struct GroupPass {
   int wbase, timer_slot;
   const uint32_t *pts_int;
   uint64_t *h;
-  uint32_t *hc;
   PhaseProf *prof;
   hipStream_t st;
   size_t nb, xw, maxent, ns0, ns1, cub = 0;
-  bool done = false;
   uint32_t *list, *dig, *tmpv, *cnt, *coff, *offsets, *ikeys0, *ivals0, *ckeys, *cidx, *flags, *pos, *ccount;
   uint16_t *tmpf;
   uint32_t *okA, *ovA, *okB, *ovB, *buckets, *Y;
   uint64_t *exp;
   void *cubtmp;
   uint8_t *filled = nullptr;  // split pipelines: bucket b holds a sum from an earlier split
-  // split pipelines: split h's accumulation waits for wait_split[h] (its points converted on the
-  // aux stream); empty: the points are resident
-  std::vector<hipEvent_t> wait_split;
   // stitch state (level ping-pong)
   const uint32_t *inK, *inV;
   size_t slots;
   uint32_t *outK, *outV, *altK, *altV;
 
   GroupPass(Device &d, const MsmShape &shape, const ScalarSlice &scal, int wb, const uint32_t *pts, uint64_t *hh,
-            uint32_t *hcc, PhaseProf *pr, hipStream_t stream, int tslot)
-      : dev(d), s(shape), sc(scal), wbase(wb), timer_slot(tslot), pts_int(pts), h(hh), hc(hcc), prof(pr),
-        st(stream) {
+            PhaseProf *pr, hipStream_t stream, int tslot)
+      : dev(d), s(shape), sc(scal), wbase(wb), timer_slot(tslot), pts_int(pts), h(hh), prof(pr), st(stream) {
     const int n = s.n;
     nb = (size_t)s.W * s.B;
     xw = xyzz_words<F>();
@@ -1128,7 +1130,7 @@ struct GroupPass {
     tmpf = dev.arena.take<uint16_t>(maxent);  // level-1 order: fine bucket within the coarse bin
     cnt = dev.arena.take<uint32_t>(s.nmat() + 1);
     coff = dev.arena.take<uint32_t>(s.nmat() + 1);
-    offsets = dev.arena.take<uint32_t>((size_t)s.NS * nb + 1);
+    offsets = dev.arena.take<uint32_t>((size_t)s.NS * (nb + 1));  // split h: offsets + h (nb + 1)
     if (s.NS > 1) filled = dev.arena.take<uint8_t>(nb);
     ns0 = stitch_slots0(s);
     ns1 = stitch_slots1(s, STITCH_BS);
@@ -1156,47 +1158,57 @@ struct GroupPass {
     if (prof && wbase == 0) prof->mark(what);
   }
 
-  void sort() {
+  // bucket sort of split sp's points [lo, hi): digits, level-1 count / scan / scatter, level 2;
+  // its entries go to the list region [W lo, W hi), its offsets to offsets + sp (nb + 1)
+  void sort(int sp) {
     const int n = s.n, c = s.c;
-    hipLaunchKernelGGL(k_digits<C>, dim3(div_up(n, 256)), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff, sc.nread,
-                       sc.mont ? 1 : 0, c, wbase, s.W, dig);
+    const int lo = (int)((int64_t)n * sp / s.NS), hi = (int)((int64_t)n * (sp + 1) / s.NS);
+    const uint32_t base = (uint32_t)((size_t)s.W * lo);
+    hipLaunchKernelGGL(k_digits<C>, dim3(div_up(hi - lo, 256)), dim3(256), 0, st, sc.data, n, lo, hi, sc.stride,
+                       sc.loff, sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig);
     ZK_CHECK(hipGetLastError());
     mark("digits");
-    const dim3 grid((unsigned)s.nwg, (unsigned)(s.W * s.NS));  // virtual windows: (split, window)
-    hipLaunchKernelGGL(k_coarse<false>, grid, dim3(256), 0, st, dig, n, s.M, s.fs, s.nbins, s.W, s.NS, cnt, tmpv,
-                       tmpf);
+    const dim3 grid((unsigned)s.nwg, (unsigned)s.W);
+    hipLaunchKernelGGL(k_coarse<false>, grid, dim3(256), 0, st, dig, n, lo, hi, s.M, s.fs, s.nbins, cnt, tmpv + base,
+                       tmpf + base);
     ZK_CHECK(hipGetLastError());
     size_t cb = cub;
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, cnt, coff, (int)(s.nmat() + 1), st));
-    hipLaunchKernelGGL(k_coarse<true>, grid, dim3(256), 0, st, dig, n, s.M, s.fs, s.nbins, s.W, s.NS, coff, tmpv,
-                       tmpf);
+    hipLaunchKernelGGL(k_coarse<true>, grid, dim3(256), 0, st, dig, n, lo, hi, s.M, s.fs, s.nbins, coff, tmpv + base,
+                       tmpf + base);
     ZK_CHECK(hipGetLastError());
     const int cap = fine_stage_cap(s.fs);
     const int lds = (4 << s.fs) + 4 * cap;
     ZK_CHECK(hipFuncSetAttribute((const void *)k_fine, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    const uint32_t nq = (uint32_t)(s.NS * s.W * s.nbins);
-    hipLaunchKernelGGL(k_fine, dim3(nq), dim3(256), lds, st, coff, s.nwg, nq, s.fs, cap, tmpv, tmpf, list, offsets);
+    const uint32_t nq = (uint32_t)(s.W * s.nbins);
+    hipLaunchKernelGGL(k_fine, dim3(nq), dim3(256), lds, st, coff, s.nwg, nq, s.fs, cap, tmpv + base, tmpf + base,
+                       list + base, offsets + (size_t)sp * (nb + 1), base);
     ZK_CHECK(hipGetLastError());
     mark("sort");
   }
 
   // accumulation of split sp: list range [offsets[sp nb], offsets[(sp+1) nb]); a run that starts
   // in a lane's chunk begins from the earlier splits' bucket sum (filled)
-  const std::atomic<int> *split_ready = nullptr;  // set by the copy thread once wait_split[h] is recorded
+  // host inputs: split h's scalars / points are on the device once the copy thread has recorded
+  // wait_sc[h] / wait_pt[h] (ready flags: an event must be recorded, in host order, before a
+  // stream waits on it)
+  std::vector<hipEvent_t> wait_sc, wait_pt;
+  const std::atomic<int> *ready_sc = nullptr, *ready_pt = nullptr;
+  void wait_for(const std::vector<hipEvent_t> &ev, const std::atomic<int> *ready, int sp) {
+    if (sp >= (int)ev.size() || !ev[sp]) return;
+    if (ready)
+      while (!ready[sp].load(std::memory_order_acquire)) std::this_thread::yield();
+    ZK_CHECK(hipStreamWaitEvent(st, ev[sp], 0));
+  }
   void accumulate(int sp) {
-    if (sp < (int)wait_split.size() && wait_split[sp]) {
-      // the event must be recorded (host order) before this stream waits on it
-      if (split_ready)
-        while (!split_ready[sp].load(std::memory_order_acquire)) std::this_thread::yield();
-      ZK_CHECK(hipStreamWaitEvent(st, wait_split[sp], 0));
-    }
+    wait_for(wait_pt, ready_pt, sp);
     if (sp == 0) timer_begin(dev, timer_slot, st);
     const size_t npts = (size_t)s.n * (sp + 1) / s.NS - (size_t)s.n * sp / s.NS;
     const size_t nsl = 2 * (((size_t)s.W * npts + s.CH - 1) / s.CH);  // <= ns0
     // upper bound on the chunk count; threads past the range's end only clear their item slots
     hipLaunchKernelGGL(k_accum<C>, dim3(div_up(nsl / 2, 256)), dim3(256), 0, st, pts_int, list,
-                       offsets + (size_t)sp * nb, (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets, ikeys0,
-                       ivals0, (uint32_t)nsl, (const uint8_t *)(sp > 0 ? filled : nullptr));
+                       offsets + (size_t)sp * (nb + 1), (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets,
+                       ikeys0, ivals0, (uint32_t)nsl, (const uint8_t *)(sp > 0 ? filled : nullptr));
     ZK_CHECK(hipGetLastError());
     if (sp == s.NS - 1) timer_end(dev, timer_slot, st);
     mark("accum");
@@ -1205,24 +1217,9 @@ struct GroupPass {
     slots = nsl;
     outK = okA; outV = ovA; altK = okB; altV = ovB;
   }
-  // split pipelines: every bucket of the split complete before the next split starts from them
-  void complete_stitch() {
-    if (done) return;
-    ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
-    stream_wait(dev, st);
-    if (*hc > (uint32_t)STITCH_BS) {
-      for (;;) {
-        if (stitch_level()) break;
-        ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
-        ZK_CHECK(hipStreamSynchronize(st));
-        if (*hc <= (uint32_t)STITCH_BS) break;
-      }
-    }
-    done = true;
-  }
   void fill_mark(int sp) {
-    hipLaunchKernelGGL(k_fill_mark, dim3(div_up(nb, 256)), dim3(256), 0, st, offsets + (size_t)sp * nb, (uint32_t)nb,
-                       sp == 0 ? 1 : 0, filled);
+    hipLaunchKernelGGL(k_fill_mark, dim3(div_up(nb, 256)), dim3(256), 0, st, offsets + (size_t)sp * (nb + 1),
+                       (uint32_t)nb, sp == 0 ? 1 : 0, filled);
     ZK_CHECK(hipGetLastError());
   }
 
@@ -1270,38 +1267,24 @@ struct GroupPass {
     ZK_CHECK(hipMemcpyAsync(h, exp, (size_t)ngrp * 4 * C::NP64 * 8, hipMemcpyDeviceToHost, st));
   }
 
-  // Levels 0..2 and the whole tail are enqueued without a host round trip: for
-  // well-spread scalars they complete every bucket.
-  static constexpr int SPECULATIVE_LEVELS = 3;
+  // Everything is enqueued without a host round trip.  The stitch levels are deterministic: a
+  // level of S item slots leaves 2 ceil(S / STITCH_BS) slots, and the level whose slots fit one
+  // block completes every run whatever the scalars (skewed inputs only make the runs longer),
+  // so all levels are launched up front (3 at BLS12-381 2^20, 4 at 2^26); with split pipelines
+  // the next split starts from complete buckets without the host looking at any count.
   void launch() {
-    sort();
     for (int sp = 0; sp < s.NS; sp++) {
+      wait_for(wait_sc, ready_sc, sp);
+      sort(sp);
       accumulate(sp);
-      done = false;
-      for (int lv = 0; lv < SPECULATIVE_LEVELS && !done; lv++) done = stitch_level();
-      if (s.NS > 1) {
-        if (sp < s.NS - 1) complete_stitch();
-        fill_mark(sp);
-      }
+      for (bool final_level = false; !final_level;) final_level = stitch_level();
+      if (s.NS > 1) fill_mark(sp);
     }
     mark("stitch");
-    if (!done) ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
     reduce_tail();
   }
-  // Only when level 2 still left more than one chunk of items (skewed scalars) does the
-  // host run further levels and redo the tail.
   void finish() {
     stream_wait(dev, st);
-    if (!done && *hc > (uint32_t)STITCH_BS) {
-      for (;;) {
-        if (stitch_level()) break;
-        ZK_CHECK(hipMemcpyAsync(hc, ccount, 4, hipMemcpyDeviceToHost, st));
-        ZK_CHECK(hipStreamSynchronize(st));
-        if (*hc <= (uint32_t)STITCH_BS) break;  // this level's stitch had one chunk: all complete
-      }
-      reduce_tail();
-      ZK_CHECK(hipStreamSynchronize(st));
-    }
     mark("export");
   }
 };
@@ -1387,9 +1370,9 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   // halve the windows per pass (the result does not depend on the grouping) down to one window
   // before giving up -- instead of aborting the caller's process on the first failed hipMalloc.
   bool dropped_twiddles = false;
-  // Host inputs in one pipeline pass: the points are split ZK_MSM_SPLITS ways, split h is
-  // accumulated as soon as its points have landed while the next split's cross PCIe
-  auto splits = [&](int wg) { return (host_inputs && wg == W && n >= ZK_MSM_SPLIT_MIN) ? ZK_MSM_SPLITS : 1; };
+  // Host inputs in one pipeline pass: the pairs are split ZK_MSM_SPLITS ways, split h is sorted
+  // and accumulated as soon as its scalars and points have landed while the next split's cross PCIe
+  auto splits = [&](int wg) { return msm_splits(n, host_inputs, wg == W); };
   MsmShape s = make_shape(n, c, Wg, splits(Wg));
   while (!dev.arena.try_reserve(sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(s))) {
     if (!dropped_twiddles) {
@@ -1408,32 +1391,38 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   ScalarSlice sc = sc_in;
   uint32_t *pts_int = nullptr;
   PhaseProf prof(st);
-  bool points_on_aux = false;
+  bool inputs_on_aux = false;
   std::thread copier;
-  std::atomic<int> split_ready[ZK_MSM_SPLITS];
+  std::atomic<int> ready_sc[ZK_MSM_SPLITS], ready_pt[ZK_MSM_SPLITS];
   if (host_inputs) {
     uint64_t *a = dev.arena.take<uint64_t>((size_t)n * sc_in.stride);
     uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
     pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
+    sc.data = a;
     // Caller memory is pageable; the runtime's pageable path runs at PCIe rate on MI355X hosts
     // (56 GB/s measured, tools/microbench/copy_bw.hip), a pinned bounce buffer only adds a host
-    // copy.  The scalars go first on the main stream (the digits and the bucket sort need only
-    // them); the points follow on the context's second stream in chunks, each converted to the
-    // internal form as soon as it lands, and the accumulation waits for the last chunk -- so
-    // the sort runs while the 96 B/pair of points are still crossing PCIe.
-    ZK_CHECK(hipMemcpyAsync(a, sc_in.data, sc_bytes, hipMemcpyHostToDevice, st));
-    sc.data = a;
-    // A copy from pageable memory returns only once it is staged, so the points are issued by a
-    // thread of their own: the calling thread goes on to enqueue the sort (and split 0's
-    // accumulation as soon as split 0's points are recorded) while the copies proceed.
+    // copy -- but a pageable copy returns only once it is staged, so the copies are issued by a
+    // thread of their own on the context's second stream, split by split (scalars, then points,
+    // converted to the internal form chunk by chunk as they land), each recording an event.  The
+    // calling thread enqueues split h's sort behind its scalars and its accumulation behind its
+    // points, so split h is sorted and accumulated while split h+1 still crosses PCIe.
     hipStream_t st2 = dev.aux_stream();
-    for (int h = 0; h < NS; h++) dev.split_event(h);  // created here, before the thread uses them
-    for (int h = 0; h < NS; h++) split_ready[h].store(0, std::memory_order_relaxed);
-    copier = std::thread([&dev, st2, NS, n, b, points, pts_int, &split_ready] {
+    for (int h = 0; h < 2 * NS; h++) dev.split_event(h);  // created here, before the thread uses them
+    for (int h = 0; h < NS; h++) {
+      ready_sc[h].store(0, std::memory_order_relaxed);
+      ready_pt[h].store(0, std::memory_order_relaxed);
+    }
+    const int stride = sc_in.stride;
+    const uint64_t *sc_host = sc_in.data;
+    copier = std::thread([&dev, st2, NS, n, a, b, stride, sc_host, points, pts_int, &ready_sc, &ready_pt] {
       ZK_CHECK(hipSetDevice(dev.id));
       const int chunk = 1 << 17;  // points per copy chunk (12 MiB of BLS12-381 points)
       for (int h = 0; h < NS; h++) {
         const int lo = (int)((int64_t)n * h / NS), hi = (int)((int64_t)n * (h + 1) / NS);
+        ZK_CHECK(hipMemcpyAsync(a + (size_t)lo * stride, sc_host + (size_t)lo * stride,
+                                (size_t)(hi - lo) * stride * 8, hipMemcpyHostToDevice, st2));
+        ZK_CHECK(hipEventRecord(dev.split_event(2 * h), st2));
+        ready_sc[h].store(1, std::memory_order_release);
         for (int p0 = lo; p0 < hi; p0 += chunk) {
           const int cnt = std::min(chunk, hi - p0);
           const size_t off = (size_t)p0 * 2 * C::NP64;
@@ -1442,11 +1431,11 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
                              pts_int + (size_t)p0 * aff_words<F>());
           ZK_CHECK(hipGetLastError());
         }
-        ZK_CHECK(hipEventRecord(dev.split_event(h), st2));
-        split_ready[h].store(1, std::memory_order_release);
+        ZK_CHECK(hipEventRecord(dev.split_event(2 * h + 1), st2));
+        ready_pt[h].store(1, std::memory_order_release);
       }
     });
-    points_on_aux = true;
+    inputs_on_aux = true;
   } else {
     pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
     hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, points, n, pts_int);
@@ -1456,7 +1445,6 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   const size_t mark = dev.arena.used();
   const size_t per_w = (size_t)c * 4 * C::NP64;  // exported u64 per window
   uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging((size_t)W * per_w * 8 + 64));
-  uint32_t *hc = reinterpret_cast<uint32_t *>(h + (size_t)W * per_w);  // stitch item count
   // Window groups run one after the other on the device's stream.  (Running two groups
   // concurrently on two streams -- one's sort and latency-bound tail beside the other's
   // accumulation -- was measured and does not pay: the two accumulations overlap each
@@ -1464,17 +1452,18 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   for (int wbase = 0; wbase < W; wbase += Wg) {
     dev.arena.rewind(mark);
     const MsmShape sg = (wbase + Wg <= W) ? s : make_shape(n, c, W - wbase);
-    GroupPass<C> pass(dev, sg, sc, wbase, pts_int, h + (size_t)wbase * per_w, hc, &prof, st, wbase == 0 ? 0 : -1);
-    if (points_on_aux) {  // joined once: later groups follow on the same stream
-      if (sg.NS == NS) {
-        for (int h = 0; h < NS; h++) pass.wait_split.push_back(dev.split_event(h));
-        pass.split_ready = split_ready;
-      } else {  // (one split pipeline per call: only a single-pass shape is split)
-        if (copier.joinable()) copier.join();
-        pass.wait_split.assign(1, dev.split_event(NS - 1));
+    GroupPass<C> pass(dev, sg, sc, wbase, pts_int, h + (size_t)wbase * per_w, &prof, st, wbase == 0 ? 0 : -1);
+    if (inputs_on_aux) {  // joined by the first group: later groups follow on the same stream
+      // (only a single-pass shape is split, so the first group has the splits of the copies)
+      ZK_REQUIRE(sg.NS == NS, "msm: split pipeline shape mismatch (internal)");
+      for (int h = 0; h < NS; h++) {
+        pass.wait_sc.push_back(dev.split_event(2 * h));
+        pass.wait_pt.push_back(dev.split_event(2 * h + 1));
       }
+      pass.ready_sc = ready_sc;
+      pass.ready_pt = ready_pt;
     }
-    points_on_aux = false;
+    inputs_on_aux = false;
     pass.launch();
     if (copier.joinable()) copier.join();  // every copy is issued (the stream order does the rest)
     pass.finish();
@@ -1503,7 +1492,7 @@ size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int windo
   const size_t sc_bytes = host_inputs ? (size_t)n * nl * 8 : 0;
   const size_t pt_bytes = host_inputs ? (size_t)n * 2 * C::NP64 * 8 : 0;
   const size_t int_bytes = (size_t)n * aff_words<F>() * 4;
-  const int NS = (host_inputs && Wg == W && n >= ZK_MSM_SPLIT_MIN) ? ZK_MSM_SPLITS : 1;
+  const int NS = msm_splits(n, host_inputs, Wg == W);
   return sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(make_shape(n, c, Wg, NS));
 }
 

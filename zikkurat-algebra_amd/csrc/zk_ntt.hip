@@ -17,7 +17,6 @@
 // output straight to its natural index k = sum_q k_q T_q (no bit-reversal pass).
 // Inverse: w -> w^-1 and the 1/N factor folded into pass 0's twiddle table.
 // Twiddle tables are built on the device once per (curve, m, gen, direction) and cached.
-#include <sys/mman.h>
 #include <algorithm>
 #include <atomic>
 #include <map>
@@ -601,30 +600,6 @@ static TwSet &twiddles(Device &dev, int curve, int m, const uint64_t *gen_mont, 
   return g_tw.emplace(key, ts).first->second;
 }
 
-// The caller's output array is often freshly allocated (the Haskell binding allocates a new
-// FlatArray per call, Poly.hs:405,417): its first touch (page faults, ~13 GB/s) would otherwise
-// happen inside the device-to-host copy.  The pages are populated for writing -- contents
-// untouched, so in-place calls are safe -- by host threads while the input copy and the passes
-// run.  (MADV_POPULATE_WRITE, Linux >= 5.14; on older kernels the call fails and nothing changes.)
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23
-#endif
-static void prefault_for_write(void *p, size_t bytes, std::vector<std::thread> &threads) {
-  if (bytes < ((size_t)4 << 20)) return;
-  const size_t page = 4096;
-  const uintptr_t lo = (uintptr_t)p & ~(uintptr_t)(page - 1);
-  const uintptr_t hi = ((uintptr_t)p + bytes + page - 1) & ~(uintptr_t)(page - 1);
-  const size_t span = hi - lo;
-  const int nt = span >= ((size_t)64 << 20) ? 8 : 1;
-  const size_t part = ((span / nt) + page - 1) & ~(page - 1);
-  for (int k = 0; k < nt; k++) {
-    const uintptr_t a = lo + k * part;
-    if (a >= hi) break;
-    const size_t len = std::min<size_t>(part, hi - a);
-    threads.emplace_back([a, len] { (void)madvise((void *)a, len, MADV_POPULATE_WRITE); });
-  }
-}
-
 struct CfgBN { using Fd = BN_Fr; using Fh = zkh::BN_Fr; };
 struct CfgBLS { using Fd = BLS_Fr; using Fh = zkh::BLS_Fr; };
 
@@ -741,12 +716,10 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   dev.arena.reset();
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
-  std::vector<std::thread> prefault;
   if (host_io) {
     uint64_t *a = dev.arena.take<uint64_t>(N * F::N64);
     d_src = a;
     d_dst = dev.arena.take<uint64_t>(N * F::N64);
-    prefault_for_write(dst, N * elbytes, prefault);
     if (sp) {
       for (Device *hk : sp->helpers) {  // chunk staging on every helper
         size_t off, len, mx = 0;
@@ -814,7 +787,10 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     T <<= r;
   }
   if (host_io) {
-    for (auto &t : prefault) t.join();
+    // (A fresh caller array pays its first touch -- ~26 ms per 512 MiB on the MI355X host --
+    // inside this copy; populating the pages from host threads during the passes, or staging
+    // the copy through pinned chunks copied out by 8 threads, measured no gain:
+    // profiles/r03e_split_e2e.txt.)
     if (sp) {
       stream_wait(dev, st);
       spread_out(dev, *sp, dst, d_dst, N * elbytes);

@@ -3,6 +3,8 @@
 #include <atomic>
 #include <chrono>
 #include <map>
+#include <algorithm>
+#include <cstring>
 #include <thread>
 
 namespace zk {

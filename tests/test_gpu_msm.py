@@ -34,7 +34,9 @@ def test_golden_jacobian(gpu, reference, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
-@pytest.mark.parametrize("window", [4, 5, 9, 13, 16, 20])
+# c = 1..3 and > 24 are clamped into 4..24 by the `_variable` entry (the reference takes 1..64,
+# bls12_381_G1_proj.c:509); the result does not depend on the window, so every c must give the same sum
+@pytest.mark.parametrize("window", [1, 3, 4, 5, 9, 13, 16, 20, 21, 22, 24, 30, 64])
 def test_window_independence(gpu, oracle, curve, window):
     sc = oracle.to_std(FR_FLD[curve], gpu.gen_fr(curve, 31, 3000))
     pts = gpu.gen_points(curve, 32, 3000)

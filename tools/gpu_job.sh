@@ -15,6 +15,7 @@
 #   ceiling   tools/microbench/valu_ceiling (prebuilt) -> gpurun_out/TAG_ceiling.json
 #   ext       tools/bench_ext.py                  -> gpurun_out/TAG_ext.json
 #   phases    MSM phase profile at several sizes  -> gpurun_out/TAG_phases.txt
+#   profsmall rocprofv3 --kernel-trace (per-dispatch timeline) of BLS12-381 2^16 MSMs -> gpurun_out/TAG_profsmall/
 #   cmd       bash tools/job_cmd.sh (scratch commands of the current experiment) -> gpurun_out/TAG_cmd.log
 set -o pipefail
 TAG=$1
@@ -45,6 +46,8 @@ for step in "$@"; do
     ceiling) timeout -k 10 120 tools/microbench/valu_ceiling > ${O}_ceiling.json 2> ${O}_ceiling.err ;;
     ext) timeout -k 10 400 python -u tools/bench_ext.py > ${O}_ext.json 2> ${O}_ext.err ;;
     phases) timeout -k 10 300 python -u tools/sweep_window.py phases > ${O}_phases.txt 2>&1 ;;
+    profsmall) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${O}_profsmall -o run --output-format csv -- \
+              python3 tools/sweep_window.py bls12_381 16 > ${O}_profsmall.log 2>&1 ;;
     cmd) timeout -k 10 ${JOB_TIMEOUT:-400} bash tools/job_cmd.sh > ${O}_cmd.log 2>&1 ;;
     *) echo "unknown step $step"; false ;;
   esac

@@ -10,6 +10,10 @@
 #include <stdint.h>
 #include <string.h>
 #include "zk_params.inc"
+#include "zk_host_adx.inc"
+#if defined(__x86_64__)
+#include <cpuid.h>
+#endif
 
 namespace zkh {
 
@@ -62,54 +66,91 @@ template <class F> inline void sub_p(uint64_t *x) {
     br = (uint64_t)(d >> 64) & 1;
   }
 }
+// Branch-free modular add / sub (the chain of doublings in finish_host is latency-bound; a
+// data-dependent compare-and-subtract branch mispredicts on random values).  p has a spare top
+// bit, so a + b < 2p never carries out.
 template <class F> inline void add(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
-  uint64_t c = 0;
-  for (int i = 0; i < F::N; i++) {
-    u128 s = (u128)a.v[i] + b.v[i] + c;
-    r.v[i] = (uint64_t)s;
-    c = (uint64_t)(s >> 64);
+  constexpr int N = F::N;
+  uint64_t s[N], d[N], c = 0, br = 0;
+  for (int i = 0; i < N; i++) {
+    const u128 x = (u128)a.v[i] + b.v[i] + c;
+    s[i] = (uint64_t)x;
+    c = (uint64_t)(x >> 64);
   }
-  if (geq_p<F>(r.v)) sub_p<F>(r.v);  // spare top bits: no carry out
+  for (int i = 0; i < N; i++) {
+    const u128 y = (u128)s[i] - F::P[i] - br;
+    d[i] = (uint64_t)y;
+    br = (uint64_t)(y >> 64) & 1;
+  }
+  const uint64_t keep = 0 - br;  // all ones: s < p, keep s
+  for (int i = 0; i < N; i++) r.v[i] = (s[i] & keep) | (d[i] & ~keep);
 }
 template <class F> inline void sub(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
-  uint64_t br = 0;
-  for (int i = 0; i < F::N; i++) {
-    u128 d = (u128)a.v[i] - b.v[i] - br;
-    r.v[i] = (uint64_t)d;
-    br = (uint64_t)(d >> 64) & 1;
+  constexpr int N = F::N;
+  uint64_t d[N], br = 0, c = 0;
+  for (int i = 0; i < N; i++) {
+    const u128 x = (u128)a.v[i] - b.v[i] - br;
+    d[i] = (uint64_t)x;
+    br = (uint64_t)(x >> 64) & 1;
   }
-  if (br) {
-    uint64_t c = 0;
-    for (int i = 0; i < F::N; i++) {
-      u128 s = (u128)r.v[i] + F::P[i] + c;
-      r.v[i] = (uint64_t)s;
-      c = (uint64_t)(s >> 64);
-    }
+  const uint64_t mask = 0 - br;  // a < b: add p back
+  for (int i = 0; i < N; i++) {
+    const u128 y = (u128)d[i] + (F::P[i] & mask) + c;
+    r.v[i] = (uint64_t)y;
+    c = (uint64_t)(y >> 64);
   }
+}
+// t (N words, value < 2p, plus a carry word `hi` in {0, 1}) -> canonical, branch-free
+template <class F> inline void reduce_once(uint64_t *r, const uint64_t *t, uint64_t hi) {
+  constexpr int N = F::N;
+  uint64_t d[N], br = 0;
+  for (int i = 0; i < N; i++) {
+    const u128 y = (u128)t[i] - F::P[i] - br;
+    d[i] = (uint64_t)y;
+    br = (uint64_t)(y >> 64) & 1;
+  }
+  const uint64_t keep = 0 - (br & (hi ^ 1));  // t < p and no carry word: keep t
+  for (int i = 0; i < N; i++) r[i] = (t[i] & keep) | (d[i] & ~keep);
 }
 template <class F> inline void neg(Fe<F> &r, const Fe<F> &a) {
   Fe<F> z;
   set_zero(z);
   sub(r, z, a);
 }
-// Montgomery product (CIOS, 64-bit limbs)
-template <class F> inline void mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+// ADX + BMI2 on this CPU (CPUID leaf 7: EBX bits 19 and 8), checked once
+inline bool cpu_has_adx() {
+#if defined(__x86_64__)
+  static const bool v = [] {
+    unsigned a, b, c, d;
+    if (!__get_cpuid_count(7, 0, &a, &b, &c, &d)) return false;
+    return (b & (1u << 19)) != 0 && (b & (1u << 8)) != 0;
+  }();
+  return v;
+#else
+  return false;
+#endif
+}
+// Montgomery product (CIOS, 64-bit limbs), fully unrolled so t stays in registers; p's top
+// word leaves a spare bit, so t < 2p fits N + 1 words and the extra carry word is at most 1
+template <class F> inline void mul_cios(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
   constexpr int N = F::N;
-  uint64_t t[N + 2];
-  memset(t, 0, sizeof t);
+  uint64_t t[N + 2] = {0};
+#pragma clang loop unroll(full)
   for (int i = 0; i < N; i++) {
     uint64_t c = 0;
+#pragma clang loop unroll(full)
     for (int j = 0; j < N; j++) {
-      u128 x = (u128)a.v[j] * b.v[i] + t[j] + c;
+      const u128 x = (u128)a.v[j] * b.v[i] + t[j] + c;
       t[j] = (uint64_t)x;
       c = (uint64_t)(x >> 64);
     }
     u128 s = (u128)t[N] + c;
     t[N] = (uint64_t)s;
     t[N + 1] = (uint64_t)(s >> 64);
-    uint64_t m = t[0] * F::MINV;
+    const uint64_t m = t[0] * F::MINV;
     u128 x = (u128)m * F::P[0] + t[0];
     c = (uint64_t)(x >> 64);
+#pragma clang loop unroll(full)
     for (int j = 1; j < N; j++) {
       x = (u128)m * F::P[j] + t[j] + c;
       t[j - 1] = (uint64_t)x;
@@ -119,17 +160,17 @@ template <class F> inline void mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
     t[N - 1] = (uint64_t)s;
     t[N] = t[N + 1] + (uint64_t)(s >> 64);
   }
-  memcpy(r.v, t, sizeof r.v);
-  if (t[N] || geq_p<F>(r.v)) sub_p<F>(r.v);
+  reduce_once<F>(r.v, t, t[N]);
 }
 // Montgomery square (SOS): the 2N-word square with every cross product once, doubled,
 // then N reduction rows -- N(N+1)/2 + N^2 word products instead of 2N^2
-template <class F> inline void sqr(Fe<F> &r, const Fe<F> &a) {
+template <class F> inline void sqr_sos(Fe<F> &r, const Fe<F> &a) {
   constexpr int N = F::N;
-  uint64_t t[2 * N + 1];
-  memset(t, 0, sizeof t);
+  uint64_t t[2 * N + 1] = {0};
+#pragma clang loop unroll(full)
   for (int i = 0; i < N; i++) {
     uint64_t c = 0;
+#pragma clang loop unroll(full)
     for (int j = i + 1; j < N; j++) {
       const u128 x = (u128)a.v[i] * a.v[j] + t[i + j] + c;
       t[i + j] = (uint64_t)x;
@@ -137,13 +178,15 @@ template <class F> inline void sqr(Fe<F> &r, const Fe<F> &a) {
     }
     t[i + N] = c;
   }
-  uint64_t top = 0;
+  uint64_t top2 = 0;
+#pragma clang loop unroll(full)
   for (int k = 0; k < 2 * N; k++) {  // double the cross products
     const uint64_t nt = t[k] >> 63;
-    t[k] = (t[k] << 1) | top;
-    top = nt;
+    t[k] = (t[k] << 1) | top2;
+    top2 = nt;
   }
   uint64_t c = 0;
+#pragma clang loop unroll(full)
   for (int i = 0; i < N; i++) {  // diagonal
     const u128 x = (u128)a.v[i] * a.v[i] + t[2 * i] + c;
     t[2 * i] = (uint64_t)x;
@@ -152,22 +195,44 @@ template <class F> inline void sqr(Fe<F> &r, const Fe<F> &a) {
     c = (uint64_t)(y >> 64);
   }
   t[2 * N] = c;
+  uint64_t top = 0;  // carry out of the previous row into t[i + N]
+#pragma clang loop unroll(full)
   for (int i = 0; i < N; i++) {  // Montgomery reduction rows
     const uint64_t m = t[i] * F::MINV;
     uint64_t cc = 0;
+#pragma clang loop unroll(full)
     for (int j = 0; j < N; j++) {
       const u128 x = (u128)m * F::P[j] + t[i + j] + cc;
       t[i + j] = (uint64_t)x;
       cc = (uint64_t)(x >> 64);
     }
-    for (int k = i + N; cc && k <= 2 * N; k++) {
-      const u128 y = (u128)t[k] + cc;
-      t[k] = (uint64_t)y;
-      cc = (uint64_t)(y >> 64);
-    }
+    const u128 y = (u128)t[i + N] + cc + top;
+    t[i + N] = (uint64_t)y;
+    top = (uint64_t)(y >> 64);
   }
-  memcpy(r.v, t + N, sizeof r.v);
-  if (t[2 * N] || geq_p<F>(r.v)) sub_p<F>(r.v);
+  t[2 * N] += top;
+  reduce_once<F>(r.v, t + N, t[2 * N]);
+}
+
+// the MULX / ADCX / ADOX product (zk_host_adx.inc) when the CPU has it, else the portable CIOS
+template <class F> inline void mul_adx(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  static_assert(F::N == 4 || F::N == 6, "ADX products are generated for 4 and 6 words");
+  uint64_t t[F::N];
+  if constexpr (F::N == 6) mont_mul_adx_6(t, a.v, b.v, F::P, F::MINV);
+  else mont_mul_adx_4(t, a.v, b.v, F::P, F::MINV);
+  reduce_once<F>(r.v, t, 0);  // < 2p -> canonical
+}
+template <class F> inline void mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b) {
+  if constexpr (F::N == 4 || F::N == 6) {
+    if (cpu_has_adx()) return mul_adx(r, a, b);
+  }
+  mul_cios(r, a, b);
+}
+template <class F> inline void sqr(Fe<F> &r, const Fe<F> &a) {
+  if constexpr (F::N == 4 || F::N == 6) {
+    if (cpu_has_adx()) return mul_adx(r, a, a);  // faster than the portable squaring
+  }
+  sqr_sos(r, a);
 }
 
 // standard <-> Montgomery

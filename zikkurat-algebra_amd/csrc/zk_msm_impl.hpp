@@ -18,7 +18,9 @@
 //                     consecutive list entries (mixed XYZZ += affine adds), flushing
 //                     complete runs to their bucket and boundary runs as partial items
 //   3. k_stitch_blk   partial items are compacted and summed per bucket by block-level
-//                     segmented scans, level after level: no serial loop anywhere, so
+//      k_stitch_raw   segmented scans (level 0: device-wide compaction + k_stitch_blk; the
+//                     few-slot levels after it: one k_stitch_raw each, block-local packing and
+//                     a segmented tree), level after level: no serial loop anywhere, so
 //                     skewed scalars (all equal, carry windows) stay fast
 //   4. k_ysum(2)      digit split of the bucket weights into plain sums Y0, Y1
 //   5. k_jobsum_blk   the weighted Y sums by bit jobs (a block of quad-cooperative additions per job)
@@ -514,6 +516,14 @@ static __global__ void __launch_bounds__(256) k_item_flags(const uint32_t *__res
 //     next level in slot 2 blk (the block's first segment, when its run started earlier
 //     -- or when it is also the last one) or 2 blk + 1 (the last segment, when its run
 //     continues), the same layout as k_stitch with SCH = BS.
+#ifndef ZK_STITCH_RAW
+// Stitch levels after the first: 1 = one k_stitch_raw launch per level (block-local packing,
+// segmented tree reduction); 0 = device-wide compaction + k_stitch_blk as on level 0.  Level 0
+// keeps the compaction either way: there most slots are empty, and k_stitch_raw over all of them
+// (2048 blocks of 64 KB LDS at BLS12-381 2^20) measured 0.155 vs 0.067 ms for the whole stitch
+// (profiles/r03h_stitch_raw_ab.txt)
+#define ZK_STITCH_RAW 1
+#endif
 template <class C, int BS>
 __global__ void __launch_bounds__(BS) k_stitch_blk(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ idx,
                                                    const uint32_t *__restrict__ vals,
@@ -569,6 +579,114 @@ __global__ void __launch_bounds__(BS) k_stitch_blk(const uint32_t *__restrict__ 
   const uint32_t item_key = (cont_in || cont_out) ? key : nb;
   if (touches_start) okeys[2 * blk] = item_key;
   if (touches_end) okeys[2 * blk + 1] = touches_start ? nb : item_key;
+}
+
+// 5c'. block stitch level straight on the item SLOTS (no global compaction): block b takes
+//      slots [b BS, (b+1) BS), packs its valid items (key < nb) into LDS in slot order
+//      (wavefront ballots + a block prefix), and sums them per key by a segmented TREE
+//      reduction with compacted work: at step d (1, 2, 4, ...) item t adds item t + d when
+//      t's offset r inside its key segment is a multiple of 2d and t + d is still in the
+//      segment, so a segment of L items costs L - 1 additions (a Hillis-Steele scan: ~L log L)
+//      and ends up summed in its FIRST item; the adding items of a step are listed compactly,
+//      so a step costs ceil(cnt / 64) wavefront additions (writers, r = 0 mod 2d, and the items
+//      read as t + d, r = d mod 2d, never coincide, so no barrier between reads and writes).
+//      A segment that touches the block's first or last item may continue in the neighbour
+//      blocks: it becomes an item of the next level (slot 2b, or 2b + 1 for the last segment
+//      when it is not also the first); every other segment is a whole bucket run.  The final
+//      level (one block) completes everything.  Compared with compaction by a device-wide
+//      scan (k_item_flags + hipCUB + k_item_index before every level), one kernel per level.
+template <class C, int BS>
+__global__ void __launch_bounds__(BS) k_stitch_raw(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                   uint32_t nslots, uint32_t nb, int final_level,
+                                                   uint32_t *__restrict__ buckets, uint32_t *__restrict__ okeys,
+                                                   uint32_t *__restrict__ ovals) {
+  using F = typename C::Fp;
+  constexpr int XW = xyzz_words<F>();
+  constexpr int NWAVE = BS / 64;
+  __shared__ uint4 tree_lds4[BS * XW / 4];  // [BS][XW] item sums (<= 64 KB: BS is 128 for G2)
+  uint32_t *lv = reinterpret_cast<uint32_t *>(tree_lds4);
+  __shared__ uint32_t skey[BS], sstart[BS], work[BS];
+  __shared__ uint32_t wcnt[NWAVE];
+  const uint32_t t = threadIdx.x, blk = blockIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t j = blk * BS + t;
+  const uint32_t kin = j < nslots ? keys[j] : nb;
+  const bool vin = kin < nb;
+  // pack the valid items: position = valid items before this slot in the block
+  uint64_t bal = __ballot(vin);
+  if (lane == 0) wcnt[wave] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  uint32_t nv = 0, off = 0;
+#pragma unroll
+  for (int w = 0; w < NWAVE; w++) {
+    off += (uint32_t)w < wave ? wcnt[w] : 0u;
+    nv += wcnt[w];
+  }
+  if (nv == 0) {  // no items: this block's output slots stay empty
+    if (!final_level && t < 2) okeys[2 * blk + t] = nb;
+    return;
+  }
+  if (vin) {
+    const uint32_t q = off + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+    skey[q] = kin;
+    const uint4 *src = reinterpret_cast<const uint4 *>(vals + (size_t)j * XW);
+    uint4 *dst = reinterpret_cast<uint4 *>(lv + (size_t)q * XW);
+#pragma unroll
+    for (int i = 0; i < XW / 4; i++) dst[i] = src[i];
+  }
+  __syncthreads();
+  const bool valid = t < nv;
+  const uint32_t key = valid ? skey[t] : 0xffffffffu - t;  // past nv: singleton segments
+  // segment start of every item: a max-scan of the start positions
+  uint32_t st = (t == 0 || (valid && skey[t - 1] != key) || !valid) ? t : 0u;
+  sstart[t] = st;
+  __syncthreads();
+  for (uint32_t o = 1; o < (uint32_t)BS; o <<= 1) {
+    const uint32_t v = t >= o ? sstart[t - o] : 0u;
+    __syncthreads();
+    st = max(st, v);
+    sstart[t] = st;
+    __syncthreads();
+  }
+  const uint32_t r = t - st;  // offset inside the segment
+  for (uint32_t d = 1; d < nv; d <<= 1) {
+    const bool need = valid && (r & (2 * d - 1)) == 0 && t + d < nv && skey[t + d] == key;
+    bal = __ballot(need);
+    if (lane == 0) wcnt[wave] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t woff = 0, cnt = 0;
+#pragma unroll
+    for (int w = 0; w < NWAVE; w++) {
+      woff += (uint32_t)w < wave ? wcnt[w] : 0u;
+      cnt += wcnt[w];
+    }
+    if (need) work[woff + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = t;
+    __syncthreads();
+    if (cnt == 0) break;  // every segment is summed (block-uniform)
+    if (t < cnt) {        // compacted: wavefronts past cnt skip the addition
+      const uint32_t a = work[t];
+      Xyzz<F> acc, o;
+      xyzz_load(acc, lv + (size_t)a * XW);
+      xyzz_load(o, lv + (size_t)(a + d) * XW);
+      xyzz_add_red(acc, o);
+      xyzz_store(lv + (size_t)a * XW, acc);
+    }
+    __syncthreads();
+  }
+  if (!valid || r != 0) return;  // the segment's first item owns its sum
+  const bool touches_start = t == 0;
+  const bool touches_end = skey[nv - 1] == key;
+  Xyzz<F> acc;
+  xyzz_load(acc, lv + (size_t)t * XW);
+  if (final_level || (!touches_start && !touches_end)) {
+    xyzz_store(buckets + (size_t)key * XW, acc);
+    return;
+  }
+  xyzz_store(ovals + (size_t)(touches_start ? 2 * blk : 2 * blk + 1) * XW, acc);
+  if (touches_start) okeys[2 * blk] = key;
+  if (touches_end) {
+    if (touches_start) okeys[2 * blk + 1] = nb;
+    else okeys[2 * blk + 1] = key;
+  }
 }
 
 // 5a'. index compaction: the valid item slots as (key, slot index) pairs -- the XYZZ
@@ -1215,6 +1333,7 @@ struct GroupPass {
     inK = ikeys0;
     inV = ivals0;
     slots = nsl;
+    level = 0;
     outK = okA; outV = ovA; altK = okB; altV = ovB;
   }
   void fill_mark(int sp) {
@@ -1225,20 +1344,29 @@ struct GroupPass {
 
   // stitch level: compact the partial items, sum them per bucket (k_stitch_blk); true when
   // every item completed at this level
+  int level = 0;
   bool stitch_level() {
-    hipLaunchKernelGGL(k_item_flags, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, (const uint32_t *)nullptr,
-                       (uint32_t)slots, (uint32_t)nb, flags);
-    ZK_CHECK(hipGetLastError());
-    size_t cb = cub;
-    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, flags, pos, (int)slots, st));
-    const bool final_level = slots <= (size_t)STITCH_BS;  // all items fit one chunk: everything completes
+    const bool final_level = slots <= (size_t)STITCH_BS;  // all items fit one block: everything completes
     const size_t nout = final_level ? 2 : 2 * ((slots + STITCH_BS - 1) / STITCH_BS);
-    hipLaunchKernelGGL(k_item_index, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, flags, pos, (uint32_t)slots,
-                       ckeys, cidx, ccount);
-    ZK_CHECK(hipGetLastError());
-    hipLaunchKernelGGL((k_stitch_blk<C, STITCH_BS>), dim3((unsigned)(nout / 2)), dim3(STITCH_BS), 0, st, ckeys, cidx,
-                       inV, ccount, (uint32_t)nb, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV, (uint32_t)nout);
-    ZK_CHECK(hipGetLastError());
+    if (ZK_STITCH_RAW && level++ > 0) {  // one kernel per level, straight on the slots
+      hipLaunchKernelGGL((k_stitch_raw<C, STITCH_BS>), dim3((unsigned)((slots + STITCH_BS - 1) / STITCH_BS)),
+                         dim3(STITCH_BS), 0, st, inK, inV, (uint32_t)slots, (uint32_t)nb, final_level ? 1 : 0,
+                         buckets, outK, outV);
+      ZK_CHECK(hipGetLastError());
+    } else {  // device-wide compaction of the valid slots, then the Hillis-Steele block stitch
+      hipLaunchKernelGGL(k_item_flags, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, (const uint32_t *)nullptr,
+                         (uint32_t)slots, (uint32_t)nb, flags);
+      ZK_CHECK(hipGetLastError());
+      size_t cb = cub;
+      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb, flags, pos, (int)slots, st));
+      hipLaunchKernelGGL(k_item_index, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, flags, pos, (uint32_t)slots,
+                         ckeys, cidx, ccount);
+      ZK_CHECK(hipGetLastError());
+      hipLaunchKernelGGL((k_stitch_blk<C, STITCH_BS>), dim3((unsigned)(nout / 2)), dim3(STITCH_BS), 0, st, ckeys,
+                         cidx, inV, ccount, (uint32_t)nb, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV,
+                         (uint32_t)nout);
+      ZK_CHECK(hipGetLastError());
+    }
     inK = outK; inV = outV; slots = nout;
     uint32_t *tk = outK, *tv = outV;
     outK = altK; outV = altV; altK = tk; altV = tv;

@@ -4,16 +4,19 @@
 namespace zk {
 
 int msm_default_window(int n) {
-  // GPU window, from window sweeps on MI355X (profiles/r01_v5_window_sweep_*.txt):
-  // 2^10 -> 9, 2^12 -> 9, 2^14 -> 11, 2^16 -> 13, 2^18..2^24 -> 16, 2^25..2^26 -> 20.
-  // (The reference uses round(log2 n - 3.5), G1_proj.c:600; the result does not depend on
-  // the choice.)  The accumulation's cost falls with c (fewer windows) while the bucket
-  // reduction's rises with it (W * 2^(c-1) buckets): c = 16 balances them from 2^18 to 2^24.
+  // GPU window, from window x chunk sweeps on MI355X (profiles/r01_v5_window_sweep_*.txt,
+  // profiles/r03l_small_window_chunk_sweep.txt): 2^10 -> 9, 2^11..2^12 -> 10, 2^13..2^16 -> 13,
+  // 2^17..2^24 -> 16, 2^25..2^26 -> 20.  (The reference uses round(log2 n - 3.5), G1_proj.c:600;
+  // the result does not depend on the choice.)  The accumulation's cost falls with c (fewer
+  // windows) while the bucket reduction's rises with it (W * 2^(c-1) buckets); at the small sizes
+  // the odd c = 13 also gives Y-sum / job-sum shapes that fill whole blocks (2^14: 0.77 -> 0.62 ms,
+  // 2^15: 0.94 -> 0.70, 2^17: 1.36 -> 0.97 ms against the round-2 table c = lg n - 3).
   if (n <= 1) return 4;
   const int lg = ilog2((unsigned)n);
   int c;
-  if (lg <= 11) c = lg - 1;
-  else if (lg <= 17) c = lg - 3;
+  if (lg <= 10) c = lg - 1;
+  else if (lg <= 12) c = 10;
+  else if (lg <= 16) c = 13;
   else if (lg <= 24) c = 16;
   else c = 20;
   if (c < 4) c = 4;

@@ -1095,12 +1095,18 @@ static MsmShape make_shape(int n, int c, int W, int NS = 1) {
     s.nwg = (int)(((size_t)s.nsplit_max() + s.M - 1) / s.M);
   }
   // entries per thread in the level-0 accumulation: 64 at scale (~2^17+ lanes), fewer for
-  // small inputs so the serial chain per lane stays short (a lone lane's madd ~12 us)
+  // small inputs so the serial chain per lane stays short (a lone lane's madd ~12 us), and at
+  // least 8 above 2^12 points (window x chunk sweep, profiles/r03l_small_window_chunk_sweep.txt;
+  // a floor at the average bucket run, n / B, measured worse: profiles/r03k_chunk_rule_sweep.txt)
   {
     const size_t ent = (size_t)s.W * (size_t)s.nsplit_max();  // entries of one accumulation launch
-    size_t ch = ent >> 17;
-    s.CH = ch >= 64 ? 64 : (ch <= 4 ? 4 : (int)ch);
+    const size_t ch = ent >> 17, lo = n > 4096 ? 8 : 4;
+    s.CH = ch >= 64 ? 64 : (ch <= lo ? (int)lo : (int)ch);
     if (ent >= ((size_t)1 << 25)) s.CH = 128;
+    if (const char *e = getenv("ZK_MSM_CH")) {  // experiment / test hook: fixed chunk length
+      const int v = atoi(e);
+      if (v > 0) s.CH = v;
+    }
   }
   return s;
 }

@@ -256,39 +256,124 @@ __global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig
   }
 }
 
-// Level 2.  Workgroup = coarse bin q = w * nbins + b, entries [coff[q * nwg], next bin's
-// start) of the level-1 order; 2^s fine buckets (dynamic LDS: 4 B counters, then the
-// staging area).  A bin of at most `cap` entries is placed in LDS and leaves as one
-// contiguous run; a larger one (skewed scalars) is scattered directly.
-static __global__ void __launch_bounds__(256) k_fine(const uint32_t *__restrict__ coff, int nwg, uint32_t nq, int s,
-                                                     int cap, const uint32_t *__restrict__ tmpv,
-                                                     const uint16_t *__restrict__ tmpf, uint32_t *__restrict__ list,
-                                                     uint32_t *__restrict__ offsets, uint32_t base) {
+// LDS counter increments with wavefront aggregation: lanes that hit the same counter are served
+// by ONE atomic (leader = the lowest such lane) for up to 4 keys with >= 4 lanes each; the rest
+// use plain per-lane atomics.  A bin whose entries share a few fine buckets -- binary 0/1 scalar
+// vectors (one bucket per window), or the carry-only top window of c = 15 / 17 / 18 -- otherwise
+// serialises 64 same-address LDS atomics per wavefront instruction.  Uniform inputs cost one
+// ballot round (the first key has 1-2 lanes).  lds_count_agg: counting only (no return value).
+template <bool RET>
+__device__ __forceinline__ uint32_t lds_inc_agg(uint32_t *ctr, uint32_t key, bool active) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1;
+  uint32_t r = 0;
+  bool todo = active;
+  for (int it = 0; it < 4; it++) {
+    const uint64_t m = __ballot(todo);
+    if (m == 0) break;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const uint32_t lk = (uint32_t)__builtin_amdgcn_readlane((int)key, leader);  // leader is wavefront-uniform
+    const bool mine = todo && key == lk;
+    const uint64_t same = __ballot(mine);
+    const int cnt = __popcll(same);
+    if (cnt < 4) break;
+    if (RET) {
+      uint32_t base = 0;
+      if ((int)lane == leader) base = atomicAdd(&ctr[lk], (uint32_t)cnt);
+      base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+      if (mine) r = base + (uint32_t)__popcll(same & below);
+    } else if ((int)lane == leader) {
+      atomicAdd(&ctr[lk], (uint32_t)cnt);
+    }
+    if (mine) todo = false;
+  }
+  if (todo) {
+    if (RET) r = atomicAdd(&ctr[key], 1u);
+    else atomicAdd(&ctr[key], 1u);
+  }
+  return r;
+}
+
+// block-wide exclusive scan of one value per thread (BS threads, BS / 64 wavefronts): wavefront
+// scans by DPP-free shuffles, then the wavefront totals
+template <int BS>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wtot, uint32_t *total) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)x, d, 64);
+    if (lane >= d) x += o;
+  }
+  if (lane == 63) wtot[w] = x;
+  __syncthreads();
+  uint32_t off = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < BS / 64; k++) {
+    off += k < w ? wtot[k] : 0u;
+    all += wtot[k];
+  }
+  *total = all;
+  __syncthreads();
+  return off + x - v;
+}
+
+// Level 2.  Workgroup (BS threads) = coarse bin q = w * nbins + b, entries [coff[q * nwg], next
+// bin's start) of the level-1 order; 2^s fine buckets (dynamic LDS: 4 B counters, then the
+// staging area).  A bin of at most `cap` entries is placed in LDS and leaves as one contiguous
+// run; a larger one (skewed scalars) is scattered directly.  Every thread keeps FINE_ILP loads in
+// flight and the counter updates are wavefront-aggregated (lds_inc_agg): a skewed bin is walked
+// by ONE workgroup, which was latency-bound at 256 threads and one load each: with 1024 threads
+// from 2^20 points per window (bins of >= 4096 entries), binary 0/1 scalars at BLS12-381 2^20 sort
+// in 0.54 vs 1.16 ms, c = 17 at 2^22 in 3.1 vs 7.3 ms, c = 16 at 2^22 in 0.97 vs 1.23 ms.  Below
+// that the round-2 shape (256 threads, one load each, plain atomics): the wide block lost 50-60 us
+// at 2^16 and the aggregation / 4-deep loads at 256 threads ~0.1 ms at 2^18
+// (profiles/r03s_fine_sort_ab.txt, profiles/r03t_fine_sort_ab.txt).
+template <int FINE_BS, int FINE_ILP, bool AGG>
+static __global__ void __launch_bounds__(FINE_BS) k_fine(const uint32_t *__restrict__ coff, int nwg, uint32_t nq,
+                                                         int s, int cap, const uint32_t *__restrict__ tmpv,
+                                                         const uint16_t *__restrict__ tmpf,
+                                                         uint32_t *__restrict__ list, uint32_t *__restrict__ offsets,
+                                                         uint32_t base) {
   // tmpv / tmpf / list point at this split's region, which starts at list position `base`:
   // the offsets written are absolute list positions
   extern __shared__ uint32_t fh[];
-  __shared__ uint32_t part[256];
+  __shared__ uint32_t wtot[FINE_BS / 64];
   const int F = 1 << s, t = threadIdx.x;
   uint32_t *sv = fh + F;
   const uint32_t q = blockIdx.x;
   const uint32_t start = coff[(size_t)q * nwg];
   const uint32_t end = coff[(size_t)(q + 1) * nwg];  // the matrix carries one extra entry: the total
   const bool staged = end - start <= (uint32_t)cap;
-  for (int f = t; f < F; f += 256) fh[f] = 0;
+  constexpr uint32_t STEP = FINE_BS * FINE_ILP;
+  for (int f = t; f < F; f += FINE_BS) fh[f] = 0;
   __syncthreads();
-  for (uint32_t e = start + t; e < end; e += 256) atomicAdd(&fh[tmpf[e]], 1u);
+  for (uint32_t e0 = start; e0 < end; e0 += STEP) {  // block-uniform trip count (wavefront ballots inside)
+    uint32_t k[FINE_ILP];
+#pragma unroll
+    for (int j = 0; j < FINE_ILP; j++) {
+      const uint32_t e = e0 + j * FINE_BS + t;
+      k[j] = e < end ? tmpf[e] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < FINE_ILP; j++) {
+      const bool act = e0 + j * FINE_BS + t < end;
+      if (AGG) lds_inc_agg<false>(fh, k[j], act);
+      else if (act) atomicAdd(&fh[k[j]], 1u);
+    }
+  }
   __syncthreads();
   // exclusive scan of the F counters: thread t owns the contiguous span [t * per, +per)
-  const int per = (F + 255) / 256;
+  const int per = (F + FINE_BS - 1) / FINE_BS;
   uint32_t sum = 0;
-  for (int k = 0; k < per; k++) {
-    const int f = t * per + k;
+  for (int j = 0; j < per; j++) {
+    const int f = t * per + j;
     if (f < F) sum += fh[f];
   }
   uint32_t tot;
-  uint32_t run = block_excl_scan256(sum, part, &tot);
-  for (int k = 0; k < per; k++) {
-    const int f = t * per + k;
+  uint32_t run = block_excl_scan<FINE_BS>(sum, wtot, &tot);
+  for (int j = 0; j < per; j++) {
+    const int f = t * per + j;
     if (f < F) {
       const uint32_t h = fh[f];
       fh[f] = staged ? run : start + run;
@@ -298,12 +383,27 @@ static __global__ void __launch_bounds__(256) k_fine(const uint32_t *__restrict_
   }
   if (q == nq - 1 && t == 0) offsets[(size_t)nq * F] = base + end;
   __syncthreads();
+  for (uint32_t e0 = start; e0 < end; e0 += STEP) {
+    uint32_t k[FINE_ILP], v[FINE_ILP];
+#pragma unroll
+    for (int j = 0; j < FINE_ILP; j++) {
+      const uint32_t e = e0 + j * FINE_BS + t;
+      k[j] = e < end ? tmpf[e] : 0u;
+      v[j] = e < end ? tmpv[e] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < FINE_ILP; j++) {
+      const bool act = e0 + j * FINE_BS + t < end;
+      const uint32_t slot = AGG ? lds_inc_agg<true>(fh, k[j], act) : (act ? atomicAdd(&fh[k[j]], 1u) : 0u);
+      if (act) {
+        if (staged) sv[slot] = v[j];
+        else list[slot] = v[j];
+      }
+    }
+  }
   if (staged) {
-    for (uint32_t e = start + t; e < end; e += 256) sv[atomicAdd(&fh[tmpf[e]], 1u)] = tmpv[e];
     __syncthreads();
-    for (uint32_t i = t; i < end - start; i += 256) list[start + i] = sv[i];
-  } else {
-    for (uint32_t e = start + t; e < end; e += 256) list[atomicAdd(&fh[tmpf[e]], 1u)] = tmpv[e];
+    for (uint32_t i = t; i < end - start; i += FINE_BS) list[start + i] = sv[i];
   }
 }
 
@@ -1303,10 +1403,18 @@ struct GroupPass {
     ZK_CHECK(hipGetLastError());
     const int cap = fine_stage_cap(s.fs);
     const int lds = (4 << s.fs) + 4 * cap;
-    ZK_CHECK(hipFuncSetAttribute((const void *)k_fine, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     const uint32_t nq = (uint32_t)(s.W * s.nbins);
-    hipLaunchKernelGGL(k_fine, dim3(nq), dim3(256), lds, st, coff, s.nwg, nq, s.fs, cap, tmpv + base, tmpf + base,
-                       list + base, offsets + (size_t)sp * (nb + 1), base);
+    if ((size_t)(hi - lo) >= (size_t)s.nbins * 4096) {  // bins of >= 4096 entries: the wide workgroup
+      ZK_CHECK(hipFuncSetAttribute((const void *)k_fine<1024, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   lds));
+      hipLaunchKernelGGL((k_fine<1024, 4, true>), dim3(nq), dim3(1024), lds, st, coff, s.nwg, nq, s.fs, cap,
+                         tmpv + base, tmpf + base, list + base, offsets + (size_t)sp * (nb + 1), base);
+    } else {
+      ZK_CHECK(hipFuncSetAttribute((const void *)k_fine<256, 1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   lds));
+      hipLaunchKernelGGL((k_fine<256, 1, false>), dim3(nq), dim3(256), lds, st, coff, s.nwg, nq, s.fs, cap,
+                         tmpv + base, tmpf + base, list + base, offsets + (size_t)sp * (nb + 1), base);
+    }
     ZK_CHECK(hipGetLastError());
     mark("sort");
   }

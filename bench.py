@@ -18,6 +18,8 @@ points in affine Montgomery form; inputs resident in HBM when the timed region s
     reference's own output for config 5 (tests/golden/baseline_configs.json).
   * NTT (configs[2]): BLS12-381 Fr NTT and iNTT of 2^24 elements on every rank (replicas:
     a single 2^24 transform is a few ms on one GPU); aggregate elems/s over ranks.
+  * config4 (configs[3], N = 1 only): the BN128 G1 MSM of 2^24 pairs (KZG-commit shaped), a
+    secondary line with its own parity check against the reference's output.
 Rank 0 at N = 1 also reports the rate through the reference-named entry points with host
 buffers (what the Haskell binding pays: PCIe included) and the reference's own C
 (oracle/_ref, lib/cbits compiled in place) timed on one host core.
@@ -57,6 +59,7 @@ def parse():
     ap.add_argument("--ntt-steps", type=int, default=5)
     ap.add_argument("--no-ntt", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) rates")
+    ap.add_argument("--no-config4", action="store_true", help="skip the secondary BN128 2^24 (config 4) MSM line")
     ap.add_argument("--cpu-msm-log", type=int, default=20, help="log2 pairs of the CPU baseline MSM")
     ap.add_argument("--cpu-ntt-log", type=int, default=20, help="log2 size of the CPU baseline NTT sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -253,6 +256,8 @@ def main():
 
     if not args.no_ntt:
         result["ntt"] = bench_ntt(zk, args, dist)
+    if rank == 0 and world == 1 and curve == "bls12_381" and not args.no_config4:
+        result["config4"] = bench_config4(zk)
     if rank == 0 and world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(zk, curve, scalars, points, ms_per_step, result.get("ntt"), args, aff)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -303,6 +308,33 @@ def msm_rooflines(curve, n, c, accum_s):
                             "iteration); half-rate ops = 1 slot, full-rate 32-bit ops = 1/2 slot",
         }
     return out
+
+
+def bench_config4(zk, steps=3, warmup=1):
+    """Secondary line at N = 1: BASELINE configs[3], the BN128 G1 MSM of 2^24 pairs (KZG-commit
+    shaped, examples/KZG.hs:77-81), device-resident, with parity against the reference's own
+    output for that config (tests/golden/baseline_configs.json)."""
+    curve, log_n = "bn128", 24
+    n, seed = 1 << log_n, SEED["bn128"]
+    t = time.time()
+    d_s, d_p = zk.DeviceBuffer(zk.gen_fr(curve, seed, n)), zk.DeviceBuffer(zk.gen_points(curve, seed, n))
+    gen_s = time.time() - t
+    for _ in range(warmup):
+        zk.msm_device(curve, n, d_s, d_p)
+    zk.load().zkg_device_synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        proj = zk.msm_device(curve, n, d_s, d_p)
+    zk.load().zkg_device_synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    aff = zk.g1_to_affine(curve, proj)
+    cfg = baseline().get("config4_bn128_msm_2^24")
+    parity = ([int(x) for x in aff] == cfg["affine"]) if cfg and cfg["seed"] == seed and cfg["log_n"] == log_n else None
+    d_s.free()
+    d_p.free()
+    return {"workload": "bn128_g1_msm_2^24", "unit": "pairs/s", "value": n / dt, "ms": dt * 1e3, "steps": steps,
+            "warmup": warmup, "window_c": zk.load().zkg_msm_default_window(n), "parity_vs_reference": parity,
+            "input_gen_s": gen_s}
 
 
 def bench_ntt(zk, args, dist):

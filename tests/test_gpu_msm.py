@@ -76,19 +76,28 @@ def test_skewed_large_vs_reference(gpu, reference, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
-@pytest.mark.parametrize("window", [0, 17])
-def test_binary_scalars_vs_oracle(gpu, oracle, curve, window):
+@pytest.mark.parametrize("window,logn", [(0, 18), (0, 20), (17, 18)])
+def test_binary_scalars_vs_oracle(gpu, oracle, curve, window, logn):
     """0/1 coefficient vectors (selector-like polynomials): every nonzero entry lands in ONE
-    bucket of window 0, i.e. one level-2 sort bin of ~n/2 entries (wavefront-aggregated counters
-    in k_fine); c = 17 adds the carry-only top window of BLS12-381 Montgomery scalars"""
-    n = 1 << 18
+    bucket of window 0, i.e. one level-2 sort bin of ~n/2 entries (2^20: the 1024-thread k_fine
+    with wavefront-aggregated counters; 2^18: the 256-thread one); c = 17 adds the carry-only
+    top window of BLS12-381 Montgomery scalars"""
+    n = 1 << logn
     rng = np.random.default_rng(91)
     sc = np.zeros((n, 4), dtype=np.uint64)
     sc[:, 0] = rng.integers(0, 2, n).astype(np.uint64)
     pts = gpu.gen_points(curve, 92, n)
     want = oracle.normalize(curve, oracle.msm(curve, sc, pts, mont=False, out="proj"))
-    assert np.array_equal(gpu.msm_variable(curve, sc, pts, window) if window else
-                          oracle.normalize(curve, gpu.msm_std(curve, sc, pts)), want)
+    if window:
+        got = gpu.msm_variable(curve, sc, pts, window)
+    elif logn >= 20:  # device-resident: one pipeline pass over all 2^20 points (host buffers split them)
+        ds, dp = gpu.DeviceBuffer(sc), gpu.DeviceBuffer(pts)
+        got = oracle.normalize(curve, gpu.msm_device(curve, n, ds, dp, mont=False))
+        ds.free()
+        dp.free()
+    else:
+        got = oracle.normalize(curve, gpu.msm_std(curve, sc, pts))
+    assert np.array_equal(got, want)
     if window:  # Montgomery scalars through the default entry: the full 255/254-bit recoding
         msc = gpu.gen_fr(curve, 93, n)
         assert np.array_equal(gpu.msm_variable(curve, oracle.to_std(FR_FLD[curve], msc), pts, window),

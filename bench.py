@@ -171,6 +171,12 @@ def main():
     from sharded import shard_range
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and args.backend == "nccl":
+        # torch ships its own HIP runtime (torch/lib/libamdhip64.so, libhsa-runtime64.so).  Loaded
+        # after the library's (/opt/rocm), it finds no GPU (two HSA runtimes in one process); loaded
+        # first, the library binds to the same runtime by soname (profiles/r03y_torch_runtime_order.txt).
+        import torch
+        torch.cuda.set_device(local % torch.cuda.device_count())
     zk.require_gpu()
     device = local % zk.device_count()  # (several ranks share a GPU only in single-GPU rehearsals)
     dist = Dist(args, device)

@@ -9,20 +9,25 @@
 Workloads (synthetic, deterministic generator zk_gen.cpp: uniform Fr scalars in Montgomery
 form -- the Haskell `msm` path -- and an arithmetic progression of random order-r subgroup
 points in affine Montgomery form; inputs resident in HBM when the timed region starts):
-  * N = 1: BASELINE configs[1], BLS12-381 G1 MSM of 2^20 pairs.  A step is one complete MSM
-    (digits, bucket sort, accumulation, bucket reduction, host finish, affine output).
-  * N > 1: BASELINE configs[4], the 2^26-pair BLS12-381 MSM split into N contiguous shards
-    (sharded.shard_range); a step is every rank's shard MSM plus the all-gather of the
-    partial sums (torch.distributed "nccl" = RCCL over xGMI) and their rank-ordered sum.
-    Total work is fixed ("strong"); rank 0 checks the affine result against the
-    reference's own output for config 5 (tests/golden/baseline_configs.json).
+  * headline, every N: the BLS12-381 G1 MSM with 2^20 pairs PER GPU (BASELINE configs[1] at
+    N = 1).  At N > 1 rank r holds pairs [r 2^20, (r+1) 2^20) of one N * 2^20-pair MSM; a step
+    is every rank's chunk MSM plus the library's own exchange of the partial sums
+    (zkg_g1_msm_device_sharded: ncclAllGather over xGMI on the library's stream, rank-ordered
+    adds) -- per-GPU work fixed as N grows ("weak").  A step is one complete MSM (digits, bucket
+    sort, accumulation, bucket reduction, host finish, affine output).
+  * config5 key, every N (BASELINE configs[4]): the 2^26-pair BLS12-381 MSM split into N
+    contiguous shards (2^26 on one GPU at N = 1): total work fixed ("strong"), parity against
+    the reference's own output for that config (tests/golden/baseline_configs.json).
   * NTT (configs[2]): BLS12-381 Fr NTT and iNTT of 2^24 elements on every rank (replicas:
     a single 2^24 transform is a few ms on one GPU); aggregate elems/s over ranks.
   * config4 (configs[3], N = 1 only): the BN128 G1 MSM of 2^24 pairs (KZG-commit shaped), a
     secondary line with its own parity check against the reference's output.
+Multi-GPU processes hold ONE HIP runtime (the library's, /opt/rocm) and never import torch: the
+rendezvous is a file (sharded.rendezvous_path), barrier / max-over-ranks / the exchange are the
+library's RCCL calls.  (--backend gloo: the torch.distributed CPU rehearsal used by the tests.)
 Rank 0 at N = 1 also reports the rate through the reference-named entry points with host
 buffers (what the Haskell binding pays: PCIe included) and the reference's own C
-(oracle/_ref, lib/cbits compiled in place) timed on one host core.
+(oracle/_ref, lib/cbits compiled in place) timed on host cores at the bench sizes.
 """
 import argparse
 import glob
@@ -52,19 +57,24 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--curve", default="bls12_381", choices=["bls12_381", "bn128"])
-    ap.add_argument("--log-n", type=int, default=0,
-                    help="log2 pairs: per GPU at N = 1 (default 20), total at N > 1 (default 26)")
+    ap.add_argument("--log-n", type=int, default=20, help="log2 pairs PER GPU of the headline MSM")
     ap.add_argument("--window", type=int, default=0)
     ap.add_argument("--ntt-log", type=int, default=24)
     ap.add_argument("--ntt-steps", type=int, default=5)
     ap.add_argument("--no-ntt", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) rates")
     ap.add_argument("--no-config4", action="store_true", help="skip the secondary BN128 2^24 (config 4) MSM line")
+    ap.add_argument("--no-config5", action="store_true", help="skip the 2^26 (config 5) strong-scaling line")
+    ap.add_argument("--config5-steps", type=int, default=3)
     ap.add_argument("--cpu-msm-log", type=int, default=20, help="log2 pairs of the CPU baseline MSM")
-    ap.add_argument("--cpu-ntt-log", type=int, default=20, help="log2 size of the CPU baseline NTT sample")
+    ap.add_argument("--cpu-ntt-log", type=int, default=24, help="log2 size of the CPU baseline NTT")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="torch.distributed backend for the partial-sum exchange (nccl = RCCL over xGMI)")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="create the library's RCCL communicator even at world size 1 (one-GPU rehearsal of the "
+                         "multi-GPU code path: rendezvous, zkg_g1_msm_device_sharded, barrier, max)")
+    ap.add_argument("--backend", default="rccl", choices=["rccl", "gloo"],
+                    help="exchange between ranks: rccl = the library's own RCCL communicator over xGMI; "
+                         "gloo = torch.distributed on the CPU (rehearsals without GPUs)")
     return ap.parse_args()
 
 
@@ -108,6 +118,22 @@ def load_pmc(kernel):
     return best
 
 
+def load_rocprof_ms(kernel_prefix):
+    """average duration (ms) of the kernel whose name starts with kernel_prefix in the newest
+    committed rocprofv3 --stats summary (profiles/*kernel_stats.csv)"""
+    import csv
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*kernel_stats.csv")), key=profile_order)
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            name = row["Name"].replace("void ", "").replace("zk::", "")
+            if name.startswith(kernel_prefix):
+                return {"ms": float(row["AverageNs"]) / 1e6, "calls": int(row["Calls"]),
+                        "source": os.path.relpath(files[-1], ROOT)}
+    return None
+
+
 def valu_ceiling():
     src, d = latest_profile("*valu_ceiling*.json")
     if not d:
@@ -117,51 +143,85 @@ def valu_ceiling():
 
 
 class Dist:
-    """torch.distributed plumbing: init, barrier, max over ranks, all-gather of tiny payloads"""
+    """rank plumbing: init, barrier, max over ranks, exchange.  backend "rccl": the library's own
+    communicator (sharded.LibComm; no torch in the process); "gloo": torch.distributed on the CPU
+    (rehearsals and the CPU tests)."""
 
     def __init__(self, args, device):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.dist = None
-        self.xdev = None
-        if self.world > 1:
-            import torch
-            import torch.distributed as dist
-            if args.backend == "nccl":
-                torch.cuda.set_device(device)
-                self.xdev = "cuda"
-            dist.init_process_group(args.backend)
-            self.dist = dist
+        self.comm = None
+        if self.world > 1 or (args.backend == "rccl" and getattr(args, "force_comm", False)):
+            if args.backend == "gloo":
+                import torch.distributed as dist
+                dist.init_process_group("gloo")
+                self.dist = dist
+            else:
+                from sharded import LibComm
+                self.comm = LibComm(self.rank, self.world)
 
     def barrier(self):
-        if self.dist:
+        if self.comm:
+            self.comm.barrier()
+        elif self.dist:
             self.dist.barrier()
 
     def max(self, x):
+        if self.comm:
+            return self.comm.max(x)
         if not self.dist:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device=self.xdev or "cpu")
+        t = torch.tensor([x], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def allgather_partials(self, partial):
+        if self.comm:
+            return list(self.comm.allgather(partial))
+        from sharded import allgather_partials
+        return allgather_partials(partial)
+
     def close(self):
-        if self.dist:
+        if self.comm:
+            self.comm.close()
+        elif self.dist:
             self.dist.destroy_process_group()
 
 
 def sharded_msm_step(zk, curve, n_local, d_s, d_p, window, dist, msm_fn=None):
-    """One step of the multi-GPU MSM: this rank's shard on its GPU, all-gather of the partial
-    projective sums, rank-ordered sum on every rank.  msm_fn lets the CPU (gloo) test stand
-    in for the GPU kernel; everything else is this exact code path."""
-    from sharded import allgather_partials, combine_partials
+    """One step of the multi-GPU MSM: this rank's shard on its GPU, the exchange of the partial
+    projective sums and their rank-ordered sum, on every rank.  On GPUs with the library's
+    communicator the whole step is one call (zkg_g1_msm_device_sharded).  msm_fn lets the CPU
+    (gloo) test stand in for the GPU kernel; the shard / exchange / combine logic is the same."""
+    from sharded import combine_partials
+    if msm_fn is None and dist.comm is not None:
+        return zk.g1_to_affine(curve, dist.comm.msm_device_sharded(curve, n_local, d_s, d_p, mont=True,
+                                                                    window=window))
     partial = msm_fn() if msm_fn else zk.msm_device(curve, n_local, d_s, d_p, mont=True, window=window)
     if dist.world > 1:
-        parts = allgather_partials(partial, device=dist.xdev)
-        _, aff = combine_partials(curve, parts)
+        _, aff = combine_partials(curve, dist.allgather_partials(partial))
     else:
         aff = zk.g1_to_affine(curve, partial)
     return aff
+
+
+def timed(dist, step, steps, warmup, sync, zk=None):
+    """warmup, then exactly `steps` steps between barrier + device sync on both sides; seconds
+    per step, max over ranks, and the last step's result.  With zk: the library's kernel timer
+    covers exactly the timed steps (read it with zk.timer(enable=False) afterwards)."""
+    out = None
+    for _ in range(warmup):
+        out = step()
+    sync()
+    if zk is not None:
+        zk.timer(enable=True, reset=True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    sync()
+    return dist.max(time.perf_counter() - t0) / steps, out
 
 
 def main():
@@ -171,69 +231,43 @@ def main():
     from sharded import shard_range
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and args.backend == "nccl":
-        # torch ships its own HIP runtime (torch/lib/libamdhip64.so, libhsa-runtime64.so).  Loaded
-        # after the library's (/opt/rocm), it finds no GPU (two HSA runtimes in one process); loaded
-        # first, the library binds to the same runtime by soname (profiles/r03y_torch_runtime_order.txt).
-        import torch
-        torch.cuda.set_device(local % torch.cuda.device_count())
     zk.require_gpu()
     device = local % zk.device_count()  # (several ranks share a GPU only in single-GPU rehearsals)
+    zk.load().zkg_set_device(device)
     dist = Dist(args, device)
     world, rank = dist.world, dist.rank
-    zk.load().zkg_set_device(device)
 
     curve = args.curve
-    if world == 1:
-        log_n = args.log_n or 20
-        n_total = 1 << log_n
-        seed = SEED[curve]
-        workload = f"{curve}_g1_msm_2^{log_n}"
-        scaling = "weak"
-    else:
-        log_n = args.log_n or 26
-        n_total = 1 << log_n
-        seed = SEED_CONFIG5 if curve == "bls12_381" else SEED[curve]
-        workload = f"{curve}_g1_msm_2^{log_n}_sharded{world}"
-        scaling = "strong"
-    lo, hi = shard_range(n_total, rank, world)
-    n_local = hi - lo
+    log_n = args.log_n
+    n_local = 1 << log_n
+    n_total = n_local * world
+    seed = SEED[curve]
+    workload = f"{curve}_g1_msm_2^{log_n}" + (f"_per_gpu_x{world}" if world > 1 else "")
+    lo = rank * n_local
     t = time.time()
     scalars = zk.gen_fr(curve, seed, n_local, start=lo)
     points = zk.gen_points(curve, seed, n_local, start=lo)
     gen_s = time.time() - t
     d_s, d_p = zk.DeviceBuffer(scalars), zk.DeviceBuffer(points)
 
-    def step():
-        return sharded_msm_step(zk, curve, n_local, d_s, d_p, args.window, dist)
-
     def sync():
         zk.load().zkg_device_synchronize()
         dist.barrier()
 
-    for _ in range(args.warmup):
-        aff = step()
-    sync()
-    zk.timer(enable=True, reset=True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        aff = step()
-    sync()
-    elapsed = dist.max(time.perf_counter() - t0)
+    step_s, aff = timed(dist, lambda: sharded_msm_step(zk, curve, n_local, d_s, d_p, args.window, dist),
+                        args.steps, args.warmup, sync, zk)
     kt_ms, kt_n = zk.timer(enable=False)
 
-    ms_per_step = elapsed / args.steps * 1e3
-    value = n_total / (elapsed / args.steps)
+    ms_per_step = step_s * 1e3
+    value = n_total / step_s
     c = args.window if args.window else zk.load().zkg_msm_default_window(n_local)
-    accum_s = (kt_ms / kt_n) / 1e3 if kt_n else float("nan")
+    accum_s = dist.max((kt_ms / kt_n) / 1e3 if kt_n else float("nan"))
 
     # parity of the timed result against the reference's own output (tests/golden)
     parity = None
-    cfgs = baseline()
-    key = ("config2_bls12_381_msm_2^20" if world == 1 else "config5_bls12_381_msm_2^26") \
-        if curve == "bls12_381" else "config4_bn128_msm_2^24"
-    cfg = cfgs.get(key)
-    if cfg and cfg["log_n"] == log_n and cfg["seed"] == seed:
+    key = "config2_bls12_381_msm_2^20" if curve == "bls12_381" else "config4_bn128_msm_2^24"
+    cfg = baseline().get(key)
+    if world == 1 and cfg and cfg["log_n"] == log_n and cfg["seed"] == seed:
         parity = [int(x) for x in aff] == cfg["affine"]
 
     result = {
@@ -245,21 +279,28 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": scaling,
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32-limb Montgomery Fp (381-bit)" if curve == "bls12_381" else "u32-limb Montgomery Fp (254-bit)",
         "data": "synthetic (deterministic generator zk_gen.cpp: uniform Fr scalars in Montgomery form, "
                 "random order-r subgroup points P0+i*H in affine Montgomery form)",
-        "config": {"workload": workload, "curve": curve, "pairs_total": n_total, "pairs_per_gpu_max": n_local,
+        "config": {"workload": workload, "curve": curve, "pairs_total": n_total, "pairs_per_gpu": n_local,
                    "scalars": "Fr Montgomery (Haskell msm path)", "window_c": c,
-                   "parallelism": f"shard{world} (contiguous chunks, RCCL all-gather of partials)"
-                   if world > 1 else "single"},
+                   "parallelism": f"shard{world} (contiguous chunks; partial sums exchanged by the library's "
+                                  f"RCCL all-gather over xGMI)" if dist.comm else "single"},
         "parity_vs_reference": parity,
         "parity_key": key if parity is not None else None,
         "input_gen_s": gen_s,
     }
+    if world > 1:
+        result["parity_note"] = ("the reference has no output for a %d-pair input; config5 carries the multi-GPU "
+                                 "parity check" % n_total)
     result.update(msm_rooflines(curve, n_local, c, accum_s))
+    d_s.free()
+    d_p.free()
 
+    if not args.no_config5 and curve == "bls12_381":
+        result["config5"] = bench_config5(zk, args, dist)
     if not args.no_ntt:
         result["ntt"] = bench_ntt(zk, args, dist)
     if rank == 0 and world == 1 and curve == "bls12_381" and not args.no_config4:
@@ -268,21 +309,63 @@ def main():
         result["end_to_end"] = end_to_end(zk, curve, scalars, points, ms_per_step, result.get("ntt"), args, aff)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(zk, curve, seed, args.cpu_msm_log, args.cpu_ntt_log)
-    d_s.free()
-    d_p.free()
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.close()
 
 
-def msm_rooflines(curve, n, c, accum_s):
+def bench_config5(zk, args, dist):
+    """BASELINE configs[4]: the 2^26-pair BLS12-381 MSM split into `world` contiguous shards (the
+    whole input on one GPU at N = 1; 2^23 pairs per GPU at N = 8), through the same library call
+    as the headline.  Total work fixed ("strong"); parity against the reference's own output."""
+    from sharded import shard_range
+    curve, log_n, seed = "bls12_381", 26, SEED_CONFIG5
+    n_total = 1 << log_n
+    world, rank = dist.world, dist.rank
+    lo, hi = shard_range(n_total, rank, world)
+    t = time.time()
+    d_s = zk.DeviceBuffer(zk.gen_fr(curve, seed, hi - lo, start=lo))
+    d_p = zk.DeviceBuffer(zk.gen_points(curve, seed, hi - lo, start=lo))
+    gen_s = time.time() - t
+
+    def sync():
+        zk.load().zkg_device_synchronize()
+        dist.barrier()
+
+    step_s, aff = timed(dist, lambda: sharded_msm_step(zk, curve, hi - lo, d_s, d_p, 0, dist),
+                        args.config5_steps, 1, sync, zk)
+    kt_ms, kt_n = zk.timer(enable=False)
+    accum_s = dist.max((kt_ms / kt_n) / 1e3 if kt_n else float("nan"))
+    d_s.free()
+    d_p.free()
+    cfg = baseline().get("config5_bls12_381_msm_2^26")
+    parity = ([int(x) for x in aff] == cfg["affine"]) if cfg and cfg["seed"] == seed and cfg["log_n"] == log_n else None
+    c = zk.load().zkg_msm_default_window(hi - lo)
+    out = {"workload": f"bls12_381_g1_msm_2^26_sharded{world}", "unit": "pairs/s", "value": n_total / step_s,
+           "ms": step_s * 1e3, "n_gpus": world, "scaling": "strong (2^26 pairs in total at every N)",
+           "pairs_per_gpu_max": hi - lo, "steps": args.config5_steps, "warmup": 1, "window_c": c,
+           "kernel_ms_max_over_ranks": accum_s * 1e3, "parity_vs_reference": parity,
+           "parity_key": "config5_bls12_381_msm_2^26", "input_gen_s": gen_s,
+           "exchange": "zkg_g1_msm_device_sharded (ncclAllGather of the partial sums on the library's stream)"
+           if dist.comm else "none (one GPU)"}
+    roof = msm_rooflines(curve, hi - lo, c, accum_s, rocprof=False)
+    out["roofline"] = roof["roofline"]
+    if "valu_roofline" in roof:
+        out["valu_roofline"] = roof["valu_roofline"]
+    return out
+
+
+def msm_rooflines(curve, n, c, accum_s, rocprof=True):
     """HBM roofline (the contract's) and VALU-issue roofline of the dominant kernel, k_accum.
     Work per launch: one XYZZ mixed add per nonzero signed digit, ~n * ceil(255/c) madds
-    (BLS12-381 / BN128 scalars are < 2^255 after REDC)."""
+    (BLS12-381 / BN128 scalars are < 2^255 after REDC).  Both fractions are given for the
+    in-run HIP-event time AND for the newest committed rocprofv3 --stats average of the same
+    kernel (profiles/*kernel_stats.csv), so they can be recomputed from profiles/."""
     windows = -(-255 // c)
     madds = windows * n
     algo_bytes = MSM_BYTES_PER_PAIR[curve] * n
     pmc = load_pmc("k_accum")
+    rp = load_rocprof_ms("k_accum<" + ("BLS381" if curve == "bls12_381" else "BN254") + ">") if rocprof else None
     out = {"roofline": {"bound": "hbm", "achieved": algo_bytes / accum_s / 1e9, "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": algo_bytes / accum_s / 1e9 / HBM_PEAK_GBPS,
                         "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
@@ -292,6 +375,9 @@ def msm_rooflines(curve, n, c, accum_s):
                                             "own stream (zkg_timer_*), averaged over the timed steps",
                         "algorithmic_bytes_per_launch": algo_bytes,
                         "note": "MSM is VALU-issue bound (integer multiply-add), see valu_roofline"}}
+    if rp:
+        out["roofline"].update({"kernel_ms_rocprof": rp["ms"], "kernel_ms_rocprof_source": rp["source"],
+                                "frac_rocprof": algo_bytes / (rp["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS})
     ceil = valu_ceiling()
     isa_src, isa = latest_profile(f"*isa_k_accum_{curve}.json")
     if ceil and isa and "hot_loop" in isa:
@@ -313,6 +399,8 @@ def msm_rooflines(curve, n, c, accum_s):
             "count_source": f"{isa_src}: static instruction counts of k_accum's hot loop (one madd per "
                             "iteration); half-rate ops = 1 slot, full-rate 32-bit ops = 1/2 slot",
         }
+        if rp:
+            out["valu_roofline"]["frac_rocprof"] = madds * slots / (rp["ms"] * 1e-3) / ceil["mad_rate"]
     return out
 
 
@@ -390,6 +478,11 @@ def bench_ntt(zk, args, dist):
                     "achieved": slots / kt, "frac": slots / kt / ceil["mad_rate"],
                     "count_source": f"{isa_src}: static issue slots of every k_ntt_pass loop x its trip count "
                                     "per launch shape, summed over the passes (tools/ntt_isa_model.py)"})
+        rp = load_rocprof_ms("k_ntt_pass<BLS_Fr, 256>") if m == 24 else None
+        if rp:  # 2^24 = three 256-point passes of this kernel (forward and inverse alike)
+            r["kernel_ms_rocprof"] = 3 * rp["ms"]
+            r["kernel_ms_rocprof_source"] = rp["source"] + " (3 x the average k_ntt_pass<BLS_Fr, 256> launch)"
+            r["roofline"]["frac_rocprof"] = NTT_BYTES_PER_ELEM * n / (3 * rp["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS
         res[name] = r
     res["value"] = res["forward"]["elems_per_s"]
     # cold call: the first transform after zkg_release (working-set arena allocated and the
@@ -469,39 +562,56 @@ def end_to_end(zk, curve, scalars, points, device_ms, ntt, args, device_aff, rep
 
 
 def cpu_baseline(zk, curve, seed, msm_log, ntt_log):
-    """The reference's own C (oracle/_ref: lib/cbits compiled in place) on one host core:
-    the MSM at the bench's own size (2^20 by default, the reference's window rule c = 17)
-    and the NTT / iNTT on a bounded 2^ntt_log sample; falls back to our C restatement."""
+    """The reference's own C (oracle/_ref: lib/cbits compiled in place) at the bench sizes: the
+    MSM of the headline's 2^msm_log pairs (MSM_mont_coeff_affine_out, the reference's window rule)
+    and the BLS12-381 NTT and iNTT at 2^ntt_log (24 = the GPU line's size).  Each is the
+    reference's single-threaded C on ONE host core; the three run at the same time on three
+    cores (ctypes releases the GIL), so the wall time is the slowest one (the 2^24 inverse,
+    ~1 min), not the sum.  Falls back to our C restatement (oracle.Oracle) without oracle/_ref."""
+    import threading
     import numpy as np
     from oracle.oracle import Oracle, Reference
     impl, kind = (Reference(), "reference") if Reference.available() else (Oracle(), "port")
     n = 1 << msm_log
     sc = zk.gen_fr(curve, seed, n)
     pts = zk.gen_points(curve, seed, n)
-    t0 = time.perf_counter()
-    out = impl.msm(curve, sc, pts, mont=True, out="affine")
-    dt = time.perf_counter() - t0
-    gpu = zk.msm_affine(curve, sc, pts)
-    res = {"value": n / dt, "unit": "pairs/s", "cores": 1, "kind": kind,
-           "sample": f"the first 2^{msm_log} pairs of the {curve} G1 MSM workload through "
-                     f"{'MSM_mont_coeff_affine_out of lib/cbits' if kind == 'reference' else 'the oracle restatement'}",
-           "seconds": dt, "host_nproc": os.cpu_count(),
-           "gpu_matches_cpu": bool(np.array_equal(out, gpu))}
     m = ntt_log
     x = zk.gen_fr("bls12_381", 0x5A4B0003, 1 << m)
     sg = zk.get_fft_subgroup("bls12_381", m)
     g = sg.gen_array()
-    ntt = {}
-    for name, inv in (("forward", False), ("inverse", True)):
+    got = {}
+
+    def run(name, fn):
         t0 = time.perf_counter()
-        y = impl.ntt("bls12_381", m, g, x, inverse=inv)
-        dt = time.perf_counter() - t0
-        gy = zk.inverse_ntt(sg, x) if inv else zk.forward_ntt(sg, x)
+        y = fn()
+        got[name] = (y, time.perf_counter() - t0)
+
+    jobs = [("msm", lambda: impl.msm(curve, sc, pts, mont=True, out="affine")),
+            ("forward", lambda: impl.ntt("bls12_381", m, g, x, inverse=False)),
+            ("inverse", lambda: impl.ntt("bls12_381", m, g, x, inverse=True))]
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=run, args=j) for j in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    out, dt = got["msm"]
+    gpu = zk.msm_affine(curve, sc, pts)
+    res = {"value": n / dt, "unit": "pairs/s", "cores": 1, "kind": kind,
+           "sample": f"the whole 2^{msm_log}-pair {curve} G1 MSM of the headline through "
+                     f"{'MSM_mont_coeff_affine_out of lib/cbits' if kind == 'reference' else 'the oracle restatement'}",
+           "seconds": dt, "host_nproc": os.cpu_count(), "gpu_matches_cpu": bool(np.array_equal(out, gpu)),
+           "concurrency": "MSM, NTT and iNTT each on one core, run at the same time (wall %.1f s)" % wall}
+    ntt = {}
+    for name in ("forward", "inverse"):
+        y, dt = got[name]
+        gy = zk.inverse_ntt(sg, x) if name == "inverse" else zk.forward_ntt(sg, x)
         ntt[name] = {"value": x.shape[0] / dt, "unit": "elems/s", "seconds": dt,
                      "gpu_matches_cpu": bool(np.array_equal(y, gy))}
     res["ntt"] = dict(ntt, cores=1, kind=kind,
                       sample=f"BLS12-381 Fr {'poly_mont_ntt_forward/_inverse of lib/cbits' if kind == 'reference' else 'oracle'}"
-                             f" at 2^{m} (bench size 2^24: the reference takes ~27 s / ~78 s there, BASELINE.md)")
+                             f" of the whole 2^{m}-element input of the GPU NTT line")
     return res
 
 

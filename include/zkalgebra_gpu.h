@@ -222,6 +222,35 @@ ZKG_API int zkg_get_devices(int *ids, int cap);  /* returns the set's size; copi
  * cached NTT twiddle tables) after waiting for the calls in flight; later calls re-allocate. */
 ZKG_API void zkg_release(void);
 
+/* Multi-GPU exchange owned by the library (RCCL over xGMI, linked from /opt/rocm): one
+ * communicator per process, one process per GPU.  The reference is single-device
+ * (bls12_381_G1_proj.c:630-644); these calls shard its MSM by contiguous chunk of the pairs.
+ * Rendezvous is the caller's: rank 0 writes the 128-byte id with zkg_comm_unique_id, every rank
+ * calls zkg_comm_init with it on the device it will use (zkg_set_device first).  Every rank must
+ * make the same sequence of zkg_comm_* / *_sharded calls.  Return 0 on success, -1 on misuse
+ * (no communicator, bad arguments), else the RCCL error code (a message goes to stderr). */
+#define ZKG_COMM_ID_BYTES 128
+ZKG_API int zkg_comm_unique_id(void *out);
+ZKG_API int zkg_comm_init(int rank, int world, const void *unique_id);
+ZKG_API int zkg_comm_destroy(void);
+ZKG_API int zkg_comm_rank(void);   /* -1 without a communicator */
+ZKG_API int zkg_comm_world(void);  /* 0 without a communicator */
+/* ncclAllGather of `bytes` host bytes per rank into recv (world * bytes, rank order) */
+ZKG_API int zkg_comm_allgather(const void *send, void *recv, size_t bytes);
+ZKG_API int zkg_comm_barrier(void);
+ZKG_API int zkg_comm_max_f64(double *x);  /* in place: the maximum over ranks */
+/* every rank passes `count` projective G1 partials (3 NP u64 each, host); all ranks receive
+ * the normalised sum of the world * count partials, added in (rank, index) order */
+ZKG_API int zkg_g1_comm_sum_partials(int curve, const uint64_t *partials, int count, uint64_t *tgt_proj);
+/* Device-resident sharded MSM: this rank's chunk (npoints_local pairs, DEVICE pointers) is
+ * computed on the communicator's device as `local_shards` contiguous sub-chunks, the
+ * world * local_shards partial sums are all-gathered by ncclAllGather on the library's stream and
+ * added in (rank, sub-chunk) order; tgt_proj (HOST, 3 NP u64) receives the normalised total on
+ * every rank.  local_shards must be the same on every rank (1 = one partial per rank). */
+ZKG_API int zkg_g1_msm_device_sharded(int curve, int npoints_local, const uint64_t *d_expos, int expo_nlimbs,
+                                      int expos_mont, const uint64_t *d_grps, int window_size, int local_shards,
+                                      uint64_t *tgt_proj);
+
 /* device-resident MSM: d_expos / d_grps are DEVICE pointers (already in HBM);
  * tgt_proj is a HOST buffer of 3*NP u64 receiving the normalised projective sum. */
 ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,

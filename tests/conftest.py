@@ -39,8 +39,30 @@ def zk():
     return zkalgebra
 
 
+_COMM = []
+
+
 @pytest.fixture(scope="session")
-def gpu(zk):
+def comm(zk):
+    """the library's own RCCL communicator, world 1 (sharded.LibComm), shared by the session:
+    the process layout of bench.py --gpus N (one HIP runtime, no torch, a live communicator)"""
+    if not _COMM:
+        from sharded import LibComm
+        os.environ.setdefault("ZKG_RDZV_KEY", f"pytest_{os.getpid()}")
+        zk.load().zkg_set_device(0)
+        _COMM.append(LibComm(0, 1))
+    yield _COMM[0]
+
+
+@pytest.fixture(scope="session")
+def gpu(zk, request):
     if zk.device_count() < 1:
         pytest.fail("GPU test ran without a visible GPU")
+    if os.environ.get("ZKG_TEST_COMM") == "1":  # run every GPU test beside a live communicator
+        request.getfixturevalue("comm")
     return zk
+
+
+def pytest_sessionfinish(session, exitstatus):
+    while _COMM:
+        _COMM.pop().close()

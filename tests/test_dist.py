@@ -52,7 +52,7 @@ def _worker(rank, world, port, curve, n_total, q):
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("curve", ["bn128", "bls12_381"])
 def test_sharded_msm_gloo(oracle, zk, curve, world):
-    import torch.multiprocessing as mp
+    import multiprocessing as mp  # plain spawn: the parent (pytest) process never loads torch
     n_total = 3000 + world  # uneven split exercises shard_range
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -46,7 +46,7 @@ def _worker(rank, world, port, curve, n_total, q):
 
 @pytest.mark.parametrize("curve", ["bn128", "bls12_381"])
 def test_sharded_msm_two_ranks_one_gpu(gpu, curve):
-    import torch.multiprocessing as mp
+    import multiprocessing as mp  # plain spawn: the parent (pytest) process never loads torch
     world, n_total = 2, (1 << 16) + 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -104,6 +104,44 @@ def test_binary_scalars_vs_oracle(gpu, oracle, curve, window, logn):
                               oracle.normalize(curve, oracle.msm(curve, msc, pts, mont=True, out="proj")))
 
 
+def _skewed_scalars(gpu, curve, kind, n, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "binary":  # std 0/1: ~n/2 entries in one bucket of window 0
+        sc = np.zeros((n, 4), dtype=np.uint64)
+        sc[:, 0] = rng.integers(0, 2, n).astype(np.uint64)
+        return sc, False
+    if kind == "equal":  # every scalar equal: one bucket per window holds all n points
+        return np.tile(gpu.gen_fr(curve, seed, 1), (n, 1)), True
+    vals = gpu.gen_fr(curve, seed, 3)  # 3 values + 5 % zeros: a few buckets of ~n/3 per window
+    sc = vals[rng.integers(0, 3, n)].copy()
+    sc[rng.random(n) < 0.05] = 0
+    return sc, True
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("logn", [17, 20])
+@pytest.mark.parametrize("kind", ["binary", "equal", "mix3"])
+def test_host_split_pipeline_skewed(gpu, oracle, curve, logn, kind):
+    """Host-buffer MSMs run split pipelines from 2^17 pairs (2 splits; 4 from 2^19): split h is
+    sorted and accumulated while split h+1 crosses PCIe, and a bucket run of a later split starts
+    from the earlier splits' sum (k_fill_mark / start_run).  Skewed scalars make runs cross
+    chunk, wavefront AND split boundaries.  Checked against the device-resident call (one
+    unsplit pipeline) and, at 2^17 and for one 2^20 case, against the oracle."""
+    n = 1 << logn
+    sc, mont = _skewed_scalars(gpu, curve, kind, n, 700 + logn)
+    pts = gpu.gen_points(curve, 701 + logn, n)
+    got = gpu.msm_affine(curve, sc, pts, std=not mont)
+    ds, dp = gpu.DeviceBuffer(sc), gpu.DeviceBuffer(pts)
+    try:
+        dev = gpu.g1_to_affine(curve, gpu.msm_device(curve, n, ds, dp, mont=mont))
+    finally:
+        ds.free()
+        dp.free()
+    assert np.array_equal(got, dev)
+    if logn == 17 or (kind == "mix3" and curve == "bls12_381"):
+        assert np.array_equal(got, oracle.msm(curve, sc, pts, mont=mont))
+
+
 @pytest.mark.parametrize("curve", CURVES)
 def test_device_resident_api(gpu, curve):
     n = 5000

@@ -3,6 +3,9 @@
 #   gpurun --timeout 900 -- bash tools/gpu_job.sh TAG step [step ...]
 # Steps (each under its own timeout; the job stops at the first failure):
 #   tests     pytest -m gpu                       -> gpurun_out/TAG_tests.log
+#   testscomm pytest -m gpu beside a live world-1 RCCL communicator (bench.py --gpus N layout) -> TAG_testscomm.log
+#   testsel   pytest -m gpu -k "$TESTSEL"         -> gpurun_out/TAG_testsel.log
+#   benchcomm bench.py --force-comm (the multi-GPU code path at world 1) -> gpurun_out/TAG_benchcomm.json
 #   smoke     __graft_entry__.smoke()             -> gpurun_out/TAG_smoke.log
 #   bench     python bench.py (defaults)          -> gpurun_out/TAG_bench.json
 #   bench2    bench.py as 2 ranks on the one GPU (gloo exchange) -> gpurun_out/TAG_bench2.json
@@ -23,11 +26,17 @@ shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 O=gpurun_out/$TAG
-BENCH_SHORT="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-config4 --ntt-steps 3"
+BENCH_SHORT="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-config4 --no-config5 --ntt-steps 3"
 for step in "$@"; do
   echo "[$(date +%T)] step $step"
   case $step in
     tests) timeout -k 10 ${TESTS_TIMEOUT:-900} python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > ${O}_tests.log 2>&1 ;;
+    testscomm) ZKG_TEST_COMM=1 timeout -k 10 ${TESTS_TIMEOUT:-900} python -u -m pytest tests -x -v -m gpu --timeout 120 \
+              --timeout-method thread > ${O}_testscomm.log 2>&1 ;;
+    testsel) timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest tests -x -v -m gpu -k "$TESTSEL" --timeout 120 \
+              --timeout-method thread > ${O}_testsel.log 2>&1 ;;
+    benchcomm) timeout -k 10 300 python -u bench.py --force-comm --steps 10 --warmup 2 --no-e2e --no-cpu-baseline \
+              --no-config4 --ntt-steps 2 > ${O}_benchcomm.json 2> ${O}_benchcomm.err ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1 ;;
     bench) timeout -k 10 400 python -u bench.py > ${O}_bench.json 2> ${O}_bench.err ;;
     bench2) timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

@@ -1,18 +1,29 @@
 """Multi-GPU MSM: shard the pairs by contiguous chunk, one exchange of partial sums.
 
-The reference is single-device.  An MSM is a group sum, so it
-partitions exactly: rank r computes S_r = sum_{i in chunk r} k_i P_i on its own GPU, the
-G partial points (3*NP u64 each, 96-144 B) are all-gathered over RCCL (torch.distributed
-"nccl" backend = RCCL on ROCm, over xGMI), and every rank adds them in rank order on the
-host.  The affine result is identical for any split, so the sharded answer is bit-exact
-against the single-device one.  The payload is tiny: the exchange is latency-bound, not
-link-bandwidth-bound.
+The reference is single-device (bls12_381_G1_proj.c:630-644).  An MSM is a
+group sum, so it partitions exactly: rank r computes S_r = sum_{i in chunk r} k_i P_i on its own
+GPU, the G partial points (3*NP u64 each, 96-144 B) are all-gathered, and every rank adds them
+in rank order.  The affine result is identical for any split, so the sharded answer is
+bit-exact against the single-device one.  The payload is tiny: the exchange is latency-bound,
+not link-bandwidth-bound.  RCCL has no elliptic-curve reduction operator, so "reduce" =
+all-gather + local adds.
 
-RCCL has no elliptic-curve reduction operator, so "reduce" = all-gather + local adds.
+On GPUs the exchange is the library's own (``LibComm``: ncclAllGather from /opt/rocm's RCCL on
+the library's stream, ``zkg_g1_msm_device_sharded``), so a process holds ONE HIP runtime and no
+torch.  The rendezvous is a file: rank 0 writes the 128-byte RCCL unique id, the other ranks
+read it (``comm_init``).  ``allgather_partials`` (torch.distributed) remains for the CPU gloo
+tests, which rehearse the same shard / combine logic without a GPU.
 """
+import ctypes
+import os
+import tempfile
+import time
+
 import numpy as np
 
 import zkalgebra as zk
+
+COMM_ID_BYTES = 128
 
 
 def shard_range(n_total, rank, world):
@@ -31,7 +42,8 @@ def combine_partials(curve, partials):
 
 
 def allgather_partials(partial, device=None):
-    """all-gather one projective point (u64 words) from every rank, rank order."""
+    """all-gather one projective point (u64 words) from every rank over torch.distributed, rank
+    order (CPU gloo rehearsals; the GPU path uses LibComm)."""
     import torch
     import torch.distributed as dist
 
@@ -44,3 +56,92 @@ def allgather_partials(partial, device=None):
     dist.all_gather_into_tensor(out, t)
     host = out.cpu().numpy().view(np.uint64)
     return [host[r * words:(r + 1) * words] for r in range(world)]
+
+
+# ----------------------------------------------------------------------------- library communicator
+
+def rendezvous_path():
+    """file through which rank 0 hands the RCCL unique id to the other ranks of one launch.
+    The key defaults to (launcher pid, MASTER_PORT): every rank of a torchrun launch is a child
+    of the same agent process, and the port separates concurrent launches.  ZKG_RDZV_KEY /
+    ZKG_RDZV_DIR override it."""
+    d = os.environ.get("ZKG_RDZV_DIR") or tempfile.gettempdir()
+    key = os.environ.get("ZKG_RDZV_KEY") or f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+    return os.path.join(d, f"zkg_rdzv_{key}.id")
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc})")
+
+
+class LibComm:
+    """The library's RCCL communicator (zkg_comm_*), one per process: barrier, max over ranks,
+    sharded device-resident MSM.  Construct after zkg_set_device."""
+
+    def __init__(self, rank, world, timeout=600.0):
+        lib = zk.load()
+        self.rank, self.world = rank, world
+        uid = ctypes.create_string_buffer(COMM_ID_BYTES)
+        path = rendezvous_path()
+        if rank == 0:
+            _check(lib.zkg_comm_unique_id(uid), "zkg_comm_unique_id")
+            tmp = f"{path}.{os.getpid()}.tmp"
+            with open(tmp, "wb") as f:
+                f.write(uid.raw)
+            os.replace(tmp, path)  # atomic: readers see the whole id or nothing
+        else:
+            t0 = time.time()
+            while True:
+                try:
+                    with open(path, "rb") as f:
+                        raw = f.read()
+                    if len(raw) == COMM_ID_BYTES:
+                        break
+                except FileNotFoundError:
+                    pass
+                if time.time() - t0 > timeout:
+                    raise TimeoutError(f"rank {rank}: no RCCL unique id at {path} after {timeout:.0f} s")
+                time.sleep(0.01)
+            ctypes.memmove(uid, raw, COMM_ID_BYTES)
+        _check(lib.zkg_comm_init(rank, world, uid), "zkg_comm_init")
+        if rank == 0:  # ncclCommInitRank is collective: every rank has read the id by now
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
+
+    def barrier(self):
+        _check(zk.load().zkg_comm_barrier(), "zkg_comm_barrier")
+
+    def max(self, x):
+        v = ctypes.c_double(float(x))
+        _check(zk.load().zkg_comm_max_f64(ctypes.byref(v)), "zkg_comm_max_f64")
+        return v.value
+
+    def allgather(self, arr):
+        """host array (same shape on every rank) -> stacked array of every rank's copy"""
+        a = np.ascontiguousarray(arr)
+        out = np.empty((self.world,) + a.shape, dtype=a.dtype)
+        _check(zk.load().zkg_comm_allgather(a.ctypes.data, out.ctypes.data, a.nbytes), "zkg_comm_allgather")
+        return out
+
+    def sum_partials(self, curve, partials):
+        """(count, 3 NP) projective partials of this rank -> normalised sum over every rank's"""
+        p = np.ascontiguousarray(partials, dtype=np.uint64).reshape(-1, 3 * zk.NLIMBS_P[curve])
+        out = np.zeros(3 * zk.NLIMBS_P[curve], dtype=np.uint64)
+        _check(zk.load().zkg_g1_comm_sum_partials(zk.CURVE_ID[curve], zk._p(p), p.shape[0], zk._p(out)),
+               "zkg_g1_comm_sum_partials")
+        return out
+
+    def msm_device_sharded(self, curve, n_local, d_scalars, d_points, mont=True, window=0, nlimbs=4,
+                           local_shards=1):
+        """this rank's chunk (device buffers) -> normalised projective MSM of every rank's chunk"""
+        out = np.zeros(3 * zk.NLIMBS_P[curve], dtype=np.uint64)
+        _check(zk.load().zkg_g1_msm_device_sharded(zk.CURVE_ID[curve], n_local, d_scalars.ptr, nlimbs,
+                                                   1 if mont else 0, d_points.ptr, window, local_shards,
+                                                   zk._p(out)), "zkg_g1_msm_device_sharded")
+        return out
+
+    def close(self):
+        _check(zk.load().zkg_comm_destroy(), "zkg_comm_destroy")

@@ -61,7 +61,9 @@ EXTENSION_SYMBOLS = [
     "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
     "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_ntt_set_max_radix", "zkg_ntt_set_table_max",
     "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
-    "zkg_release",
+    "zkg_release", "zkg_comm_unique_id", "zkg_comm_init", "zkg_comm_destroy", "zkg_comm_rank", "zkg_comm_world",
+    "zkg_comm_allgather", "zkg_comm_barrier", "zkg_comm_max_f64", "zkg_g1_comm_sum_partials",
+    "zkg_g1_msm_device_sharded",
 ]
 
 _lib = None
@@ -102,6 +104,13 @@ def load():
                                           ctypes.c_void_p, U64P, U64P, ctypes.c_void_p]
         lib.zkg_arr_dot_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, U64P]
         lib.zkg_arr_powers_device.argtypes = [ctypes.c_int, ctypes.c_int, U64P, U64P, ctypes.c_void_p]
+        lib.zkg_comm_unique_id.argtypes = [ctypes.c_void_p]
+        lib.zkg_comm_init.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        lib.zkg_comm_allgather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        lib.zkg_comm_max_f64.argtypes = [ctypes.POINTER(ctypes.c_double)]
+        lib.zkg_g1_comm_sum_partials.argtypes = [ctypes.c_int, U64P, ctypes.c_int, U64P]
+        lib.zkg_g1_msm_device_sharded.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, U64P]
         _lib = lib
     return _lib
 

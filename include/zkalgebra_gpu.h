@@ -213,7 +213,12 @@ ZKG_API void zkg_device_synchronize(void);
  * own chunk over that device's PCIe link), the partial sums added in list order.  A device may
  * be listed more than once (one stream / arena per occurrence).  n <= 1: the calling thread's
  * device only (the default; also set by the environment variable ZKG_DEVICES = "all" or
- * "0,1,..." at first use).  Returns 0, or -1 (set unchanged) for an invalid id.  The
+ * "0,1,..." at first use).  A one-entry set pins the host-buffer MSMs (and NTTs) to that device.
+ * The host-buffer NTT symbols (2^16 points and up) compute on the calling thread's device when the
+ * set lists it, else on the first listed device, and move chunk k of the input / output over
+ * listed device k's PCIe link (peer copies over xGMI).  In a one-process-per-GPU job (bench.py
+ * --gpus N, or any RCCL job) leave the set empty: every rank would otherwise push its host copies
+ * through every GPU's link.  Returns 0, or -1 (set unchanged) for an invalid id.  The
  * device-resident zkg_*_device calls always run on the calling thread's device. */
 ZKG_API int zkg_set_devices(const int *ids, int n);
 ZKG_API int zkg_get_devices(int *ids, int cap);  /* returns the set's size; copies min(size, cap) ids */

@@ -57,7 +57,7 @@ for step in "$@"; do
     phases) timeout -k 10 300 python -u tools/sweep_window.py phases > ${O}_phases.txt 2>&1 ;;
     profsmall) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${O}_profsmall -o run --output-format csv -- \
               python3 tools/sweep_window.py bls12_381 16 > ${O}_profsmall.log 2>&1 ;;
-    cmd) timeout -k 10 ${JOB_TIMEOUT:-400} bash tools/job_cmd.sh > ${O}_cmd.log 2>&1 ;;
+    cmd) TAG=$TAG timeout -k 10 ${JOB_TIMEOUT:-400} bash tools/job_cmd.sh > ${O}_cmd.log 2>&1 ;;
     *) echo "unknown step $step"; false ;;
   esac
   rc=$?

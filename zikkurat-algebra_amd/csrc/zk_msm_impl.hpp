@@ -661,7 +661,7 @@ __global__ void __launch_bounds__(BS) k_stitch_blk(const uint32_t *__restrict__ 
                                                    uint32_t nout) {
   using F = typename C::Fp;
   constexpr int XW = xyzz_words<F>();
-  __shared__ uint4 stitch_lds4[BS * XW / 4];  // [BS][XW] partial sums (<= 64 KB: BS is 128 for G2)
+  __shared__ uint4 stitch_lds4[BS * XW / 4];  // [BS][XW] partial sums (64 KB + skey: > 64 KB LDS, gfx950)
   uint32_t *lv = reinterpret_cast<uint32_t *>(stitch_lds4);
   __shared__ uint32_t skey[BS];
   const uint32_t M = *count;
@@ -731,7 +731,9 @@ __global__ void __launch_bounds__(BS) k_stitch_raw(const uint32_t *__restrict__ 
   using F = typename C::Fp;
   constexpr int XW = xyzz_words<F>();
   constexpr int NWAVE = BS / 64;
-  __shared__ uint4 tree_lds4[BS * XW / 4];  // [BS][XW] item sums (<= 64 KB: BS is 128 for G2)
+  // [BS][XW] item sums: 64 KB for BLS12-381 G1 (BS 256), plus skey / sstart / work: ~67.6 KB of
+  // static LDS -- gfx950 has 160 KB per CU (the Makefile builds for gfx950 only)
+  __shared__ uint4 tree_lds4[BS * XW / 4];
   uint32_t *lv = reinterpret_cast<uint32_t *>(tree_lds4);
   __shared__ uint32_t skey[BS], sstart[BS], work[BS];
   __shared__ uint32_t wcnt[NWAVE];
@@ -1155,12 +1157,58 @@ struct MsmShape {
   // level-1 workgroups of M entries (nwg per window)
   int fs, nbins, M, nwg;
   // point splits: the entries are sorted by (split, window, bucket), split h holding the pairs
-  // [n h / NS, n (h+1) / NS); each split is accumulated by its own launch (host-input calls
+  // [split_lo(h), split_lo(h + 1)); each split is accumulated by its own launch (host-input calls
   // start on the first split while the later splits' points still cross PCIe)
   int NS;
   size_t nmat() const { return (size_t)W * nbins * nwg; }  // level-1 count matrix of one split
-  int nsplit_max() const { return (n + NS - 1) / NS; }  // points of the largest split
+  int split_lo(int h) const;
+  int split_ch(int h) const;  // accumulation chunk length of split h
+  int nsplit_max() const {  // points of the largest split
+    int m = 0;
+    for (int h = 0; h < NS; h++) m = std::max(m, split_lo(h + 1) - split_lo(h));
+    return m;
+  }
 };
+
+// Split weights of a host-input MSM (sixteenths): the first split is small so the device starts
+// after 1/8 of the copies, the last one is small so little accumulation is left after the last
+// copy lands, the middle ones are large so few splits pay the per-split sort / stitch.
+// ZK_MSM_SPLIT_W="w0,w1,..." (experiment hook, read once): other weights / split counts (<= 8).
+struct SplitCfg {
+  int ns;
+  int w[8];
+};
+static const SplitCfg &split_cfg() {
+  static const SplitCfg cfg = [] {
+    SplitCfg c{5, {2, 3, 4, 4, 3}};
+    if (const char *e = getenv("ZK_MSM_SPLIT_W")) {
+      SplitCfg d{0, {0}};
+      for (const char *p = e; *p && d.ns < 8;) {
+        char *end = nullptr;
+        const long v = strtol(p, &end, 10);
+        if (end == p || v <= 0) break;
+        d.w[d.ns++] = (int)v;
+        p = *end == ',' ? end + 1 : end;
+      }
+      if (d.ns >= 1) c = d;
+    }
+    return c;
+  }();
+  return cfg;
+}
+static const int *split_weights(int NS) {
+  return NS == split_cfg().ns ? split_cfg().w : nullptr;  // nullptr: equal splits
+}
+inline int MsmShape::split_lo(int h) const {
+  const int *w = split_weights(NS);
+  if (!w) return (int)((int64_t)n * h / NS);
+  int acc = 0, tot = 0;
+  for (int k = 0; k < NS; k++) {
+    tot += w[k];
+    if (k < h) acc += w[k];
+  }
+  return (int)((int64_t)n * acc / tot);
+}
 
 static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; return r; }
 
@@ -1168,17 +1216,15 @@ static int ilog2(unsigned x) { int r = 0; while ((1u << (r + 1)) <= x) r++; retu
 // MI355X (profiles/r01_*, profiles/r02h_qy_qa_sweep.txt): Y sums take 16 buckets per lane at
 // scale (8: ysum 0.37 -> 0.48 ms, 4: 0.66 ms at BLS12-381 2^20), the accumulation 64 sorted entries per lane (128 from 2^25
 // entries on, profiles/r01_v7_ch_sweep.txt).
-#ifndef ZK_MSM_SPLITS
-#define ZK_MSM_SPLITS 4  // most splits of a host-input MSM pipeline (copy / sort / accumulation overlap)
-#endif
-// Splits of a host-input MSM whose windows fit one pipeline pass: 4 from 2^19 pairs (splits of
-// >= 2^17 pairs keep every accumulation launch at >= 2 waves per SIMD), 2 from 2^17, else 1
-// (BLS12-381 2^20 through the reference symbol: 6.3-6.4 ms unsplit, 5.4-5.5 ms in two splits,
-// 4.8-4.9 ms in four, profiles/r03e_split_e2e.txt)
+#define ZK_MSM_SPLITS_MAX 8  // most splits of a host-input MSM pipeline (copy / sort / accumulation overlap)
+// Splits of a host-input MSM whose windows fit one pipeline pass: 5 weighted splits (2, 3, 4, 4, 3
+// sixteenths, split_weights) from 2^19 pairs, 2 from 2^17, else 1 (BLS12-381 2^20 through the
+// reference symbol: 6.3-6.4 ms unsplit, 5.4-5.5 ms in two splits, 4.8-4.9 ms in four equal ones,
+// profiles/r03e_split_e2e.txt; the round-4 copy / sort / conversion streams: profiles/r04*_e2e*)
 static int msm_splits(int n, bool host_inputs, bool one_pass) {
   if (!host_inputs || !one_pass) return 1;
-  if (n >= (1 << 19)) return ZK_MSM_SPLITS;
-  if (n >= (1 << 17)) return ZK_MSM_SPLITS < 2 ? ZK_MSM_SPLITS : 2;
+  if (n >= (1 << 19)) return split_cfg().ns;
+  if (n >= (1 << 17)) return split_cfg().ns < 2 ? split_cfg().ns : 2;
   return 1;
 }
 #ifndef ZK_YSUM_LANES
@@ -1226,17 +1272,23 @@ static MsmShape make_shape(int n, int c, int W, int NS = 1) {
   // small inputs so the serial chain per lane stays short (a lone lane's madd ~12 us), and at
   // least 8 above 2^12 points (window x chunk sweep, profiles/r03l_small_window_chunk_sweep.txt;
   // a floor at the average bucket run, n / B, measured worse: profiles/r03k_chunk_rule_sweep.txt)
-  {
-    const size_t ent = (size_t)s.W * (size_t)s.nsplit_max();  // entries of one accumulation launch
-    const size_t ch = ent >> 17, lo = n > 4096 ? 8 : 4;
-    s.CH = ch >= 64 ? 64 : (ch <= lo ? (int)lo : (int)ch);
-    if (ent >= ((size_t)1 << 25)) s.CH = 128;
-    if (const char *e = getenv("ZK_MSM_CH")) {  // experiment / test hook: fixed chunk length
-      const int v = atoi(e);
-      if (v > 0) s.CH = v;
-    }
-  }
+  s.CH = s.split_ch(0);
   return s;
+}
+
+// The chunk rule is applied to every split's own entry count (each launch keeps ~2^17 lanes = 2
+// waves per SIMD, or 2^18 at CH 64), so a small split does not run its accumulation at one wave per
+// SIMD (round 3 sized every split's chunks from the largest split).
+inline int MsmShape::split_ch(int h) const {
+  const size_t ent = (size_t)W * (size_t)(split_lo(h + 1) - split_lo(h));  // entries of this launch
+  const size_t ch = ent >> 17, lo = n > 4096 ? 8 : 4;
+  int r = ch >= 64 ? 64 : (ch <= lo ? (int)lo : (int)ch);
+  if (ent >= ((size_t)1 << 25)) r = 128;
+  if (const char *e = getenv("ZK_MSM_CH")) {  // experiment / test hook: fixed chunk length
+    const int v = atoi(e);
+    if (v > 0) r = v;
+  }
+  return r;
 }
 
 // items per workgroup of the block stitch: 128 for the wide G2 points, so the LDS exchange
@@ -1244,7 +1296,14 @@ static MsmShape make_shape(int n, int c, int W, int NS = 1) {
 template <class F>
 constexpr int stitch_bs() { return xyzz_words<F>() > 64 ? 128 : 256; }
 
-static size_t stitch_slots0(const MsmShape &s) { return 2 * (((size_t)s.W * s.nsplit_max() + s.CH - 1) / s.CH); }
+static size_t stitch_slots0(const MsmShape &s) {  // item slots of the largest split's accumulation
+  size_t m = 0;
+  for (int h = 0; h < s.NS; h++) {
+    const size_t ch = (size_t)s.split_ch(h);
+    m = std::max(m, 2 * (((size_t)s.W * (s.split_lo(h + 1) - s.split_lo(h)) + ch - 1) / ch));
+  }
+  return m;
+}
 static size_t stitch_slots1(const MsmShape &s, int bs) { return 2 * ((stitch_slots0(s) + bs - 1) / bs) + 2; }
 
 // sorted entries of one pipeline pass: passes of several windows are kept at <= 2^30 entries
@@ -1285,6 +1344,7 @@ static size_t group_bytes(const MsmShape &s) {
   add((size_t)s.W * s.NY * xw);           // Y
   add((size_t)s.W * s.J * 4 * C::NP64 * 8);  // export
   add(cub > cub2 ? cub : cub2);
+  if (s.NS > 1) add(cub > cub2 ? cub : cub2);  // the sort stream's own scan scratch
   return bytes + (1 << 20);
 }
 
@@ -1363,6 +1423,14 @@ struct GroupPass {
   uint64_t *exp;
   void *cubtmp;
   uint8_t *filled = nullptr;  // split pipelines: bucket b holds a sum from an earlier split
+  // host inputs: the sorts run on their own stream (sst, with their own scan scratch) beside the
+  // previous split's accumulation, and the points of split h (reference form, pts_ref) are
+  // converted on the main stream right before its accumulation -- the copy stream carries
+  // copies only
+  hipStream_t sst = nullptr;
+  void *cubtmp_sort = nullptr;
+  const uint64_t *pts_ref = nullptr;
+  std::vector<hipEvent_t> sorted_ev;
   // stitch state (level ping-pong)
   const uint32_t *inK, *inV;
   size_t slots;
@@ -1405,6 +1473,7 @@ struct GroupPass {
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
     if (cub2 > cub) cub = cub2;
     cubtmp = dev.arena.take<char>(cub);
+    if (s.NS > 1) cubtmp_sort = dev.arena.take<char>(cub);
   }
   void mark(const char *what) {  // the phase profile follows the first group's stream
     if (prof && wbase == 0) prof->mark(what);
@@ -1412,14 +1481,14 @@ struct GroupPass {
 
   // bucket sort of split sp's points [lo, hi): digits, level-1 count / scan / scatter, level 2;
   // its entries go to the list region [W lo, W hi), its offsets to offsets + sp (nb + 1)
-  void sort(int sp) {
+  void sort(int sp, hipStream_t st, void *cubtmp) {
     const int n = s.n, c = s.c;
-    const int lo = (int)((int64_t)n * sp / s.NS), hi = (int)((int64_t)n * (sp + 1) / s.NS);
+    const int lo = s.split_lo(sp), hi = s.split_lo(sp + 1);
     const uint32_t base = (uint32_t)((size_t)s.W * lo);
     hipLaunchKernelGGL(k_digits<C>, dim3(div_up(hi - lo, 256)), dim3(256), 0, st, sc.data, n, lo, hi, sc.stride,
                        sc.loff, sc.nread, sc.mont ? 1 : 0, c, wbase, s.W, dig);
     ZK_CHECK(hipGetLastError());
-    mark("digits");
+    if (st == this->st) mark("digits");
     const dim3 grid((unsigned)s.nwg, (unsigned)s.W);
     hipLaunchKernelGGL(k_coarse<false>, grid, dim3(256), 0, st, dig, n, lo, hi, s.M, s.fs, s.nbins, cnt, tmpv + base,
                        tmpf + base);
@@ -1444,7 +1513,7 @@ struct GroupPass {
                          tmpv + base, tmpf + base, list + base, offsets + (size_t)sp * (nb + 1), base);
     }
     ZK_CHECK(hipGetLastError());
-    mark("sort");
+    if (st == this->st) mark("sort");
   }
 
   // accumulation of split sp: list range [offsets[sp nb], offsets[(sp+1) nb]); a run that starts
@@ -1454,20 +1523,28 @@ struct GroupPass {
   // stream waits on it)
   std::vector<hipEvent_t> wait_sc, wait_pt;
   const std::atomic<int> *ready_sc = nullptr, *ready_pt = nullptr;
-  void wait_for(const std::vector<hipEvent_t> &ev, const std::atomic<int> *ready, int sp) {
+  void wait_for(hipStream_t on, const std::vector<hipEvent_t> &ev, const std::atomic<int> *ready, int sp) {
     if (sp >= (int)ev.size() || !ev[sp]) return;
     if (ready)
       while (!ready[sp].load(std::memory_order_acquire)) std::this_thread::yield();
-    ZK_CHECK(hipStreamWaitEvent(st, ev[sp], 0));
+    ZK_CHECK(hipStreamWaitEvent(on, ev[sp], 0));
+  }
+  // host inputs: split sp's points (landed in pts_ref) -> internal form, on the main stream
+  void convert(int sp) {
+    const int lo = s.split_lo(sp), hi = s.split_lo(sp + 1);
+    if (hi <= lo) return;
+    hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(hi - lo, 256)), dim3(256), 0, st,
+                       pts_ref + (size_t)lo * 2 * C::NP64, hi - lo, const_cast<uint32_t *>(pts_int) + (size_t)lo * aff_words<F>());
+    ZK_CHECK(hipGetLastError());
   }
   void accumulate(int sp) {
-    wait_for(wait_pt, ready_pt, sp);
     if (sp == 0) timer_begin(dev, timer_slot, st);
-    const size_t npts = (size_t)s.n * (sp + 1) / s.NS - (size_t)s.n * sp / s.NS;
-    const size_t nsl = 2 * (((size_t)s.W * npts + s.CH - 1) / s.CH);  // <= ns0
+    const size_t npts = (size_t)s.split_lo(sp + 1) - (size_t)s.split_lo(sp);
+    const int CH = s.split_ch(sp);
+    const size_t nsl = 2 * (((size_t)s.W * npts + CH - 1) / CH);  // <= ns0
     // upper bound on the chunk count; threads past the range's end only clear their item slots
     hipLaunchKernelGGL(k_accum<C>, dim3(div_up(nsl / 2, 256)), dim3(256), 0, st, pts_int, list,
-                       offsets + (size_t)sp * (nb + 1), (uint32_t)nb, s.CH, (uint32_t)s.W, (uint32_t)s.B, buckets,
+                       offsets + (size_t)sp * (nb + 1), (uint32_t)nb, CH, (uint32_t)s.W, (uint32_t)s.B, buckets,
                        ikeys0, ivals0, (uint32_t)nsl, (const uint8_t *)(sp > 0 ? filled : nullptr));
     ZK_CHECK(hipGetLastError());
     if (sp == s.NS - 1) timer_end(dev, timer_slot, st);
@@ -1544,8 +1621,17 @@ struct GroupPass {
   // the next split starts from complete buckets without the host looking at any count.
   void launch() {
     for (int sp = 0; sp < s.NS; sp++) {
-      wait_for(wait_sc, ready_sc, sp);
-      sort(sp);
+      if (sst) {  // split sp's sort on the sort stream, beside split sp-1's accumulation
+        wait_for(sst, wait_sc, ready_sc, sp);
+        sort(sp, sst, cubtmp_sort);
+        ZK_CHECK(hipEventRecord(sorted_ev[sp], sst));
+      } else {
+        wait_for(st, wait_sc, ready_sc, sp);
+        sort(sp, st, cubtmp);
+      }
+      wait_for(st, wait_pt, ready_pt, sp);
+      if (pts_ref) convert(sp);
+      if (sst) ZK_CHECK(hipStreamWaitEvent(st, sorted_ev[sp], 0));
       accumulate(sp);
       for (bool final_level = false; !final_level;) final_level = stitch_level();
       if (s.NS > 1) fill_mark(sp);
@@ -1640,7 +1726,7 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   // halve the windows per pass (the result does not depend on the grouping) down to one window
   // before giving up -- instead of aborting the caller's process on the first failed hipMalloc.
   bool dropped_twiddles = false;
-  // Host inputs in one pipeline pass: the pairs are split ZK_MSM_SPLITS ways, split h is sorted
+  // Host inputs in one pipeline pass: the pairs are split msm_splits() ways, split h is sorted
   // and accumulated as soon as its scalars and points have landed while the next split's cross PCIe
   auto splits = [&](int wg) { return msm_splits(n, host_inputs, wg == W); };
   MsmShape s = make_shape(n, c, Wg, splits(Wg));
@@ -1663,45 +1749,44 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   PhaseProf prof(st);
   bool inputs_on_aux = false;
   std::thread copier;
-  std::atomic<int> ready_sc[ZK_MSM_SPLITS], ready_pt[ZK_MSM_SPLITS];
+  std::atomic<int> ready_sc[ZK_MSM_SPLITS_MAX], ready_pt[ZK_MSM_SPLITS_MAX];
+  uint64_t *pts_ref = nullptr;  // host inputs: the device copy of the caller's (reference-form) points
   if (host_inputs) {
     uint64_t *a = dev.arena.take<uint64_t>((size_t)n * sc_in.stride);
     uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
     pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
     sc.data = a;
+    pts_ref = b;
     // Caller memory is pageable; the runtime's pageable path runs at PCIe rate on MI355X hosts
     // (56 GB/s measured, tools/microbench/copy_bw.hip), a pinned bounce buffer only adds a host
     // copy -- but a pageable copy returns only once it is staged, so the copies are issued by a
-    // thread of their own on the context's second stream, split by split (scalars, then points,
-    // converted to the internal form chunk by chunk as they land), each recording an event.  The
-    // calling thread enqueues split h's sort behind its scalars and its accumulation behind its
-    // points, so split h is sorted and accumulated while split h+1 still crosses PCIe.
+    // thread of their own on the context's second stream, split by split (scalars, then points),
+    // each recording an event; that stream carries nothing but copies.  The calling thread
+    // enqueues split h's sort (on the sort stream) behind its scalars, and its point conversion
+    // and accumulation (main stream) behind its points, so split h is accumulated while split h+1
+    // still crosses PCIe.  (Round 3 converted the points on the copy stream: every conversion then
+    // delayed the next copy, and ran beside an accumulation at a tenth of its speed --
+    // profiles/r04b_e2e_trace.txt.)
     hipStream_t st2 = dev.aux_stream();
-    for (int h = 0; h < 2 * NS; h++) dev.split_event(h);  // created here, before the thread uses them
+    for (int h = 0; h < 3 * NS; h++) dev.split_event(h);  // created here, before the thread uses them
     for (int h = 0; h < NS; h++) {
       ready_sc[h].store(0, std::memory_order_relaxed);
       ready_pt[h].store(0, std::memory_order_relaxed);
     }
     const int stride = sc_in.stride;
     const uint64_t *sc_host = sc_in.data;
-    copier = std::thread([&dev, st2, NS, n, a, b, stride, sc_host, points, pts_int, &ready_sc, &ready_pt] {
+    const MsmShape shp = s;
+    copier = std::thread([&dev, st2, NS, shp, a, b, stride, sc_host, points, &ready_sc, &ready_pt] {
       ZK_CHECK(hipSetDevice(dev.id));
-      const int chunk = 1 << 17;  // points per copy chunk (12 MiB of BLS12-381 points)
       for (int h = 0; h < NS; h++) {
-        const int lo = (int)((int64_t)n * h / NS), hi = (int)((int64_t)n * (h + 1) / NS);
+        const int lo = shp.split_lo(h), hi = shp.split_lo(h + 1);
         ZK_CHECK(hipMemcpyAsync(a + (size_t)lo * stride, sc_host + (size_t)lo * stride,
                                 (size_t)(hi - lo) * stride * 8, hipMemcpyHostToDevice, st2));
-        ZK_CHECK(hipEventRecord(dev.split_event(2 * h), st2));
+        ZK_CHECK(hipEventRecord(dev.split_event(3 * h), st2));
         ready_sc[h].store(1, std::memory_order_release);
-        for (int p0 = lo; p0 < hi; p0 += chunk) {
-          const int cnt = std::min(chunk, hi - p0);
-          const size_t off = (size_t)p0 * 2 * C::NP64;
-          ZK_CHECK(hipMemcpyAsync(b + off, points + off, (size_t)cnt * 2 * C::NP64 * 8, hipMemcpyHostToDevice, st2));
-          hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(cnt, 256)), dim3(256), 0, st2, b + off, cnt,
-                             pts_int + (size_t)p0 * aff_words<F>());
-          ZK_CHECK(hipGetLastError());
-        }
-        ZK_CHECK(hipEventRecord(dev.split_event(2 * h + 1), st2));
+        const size_t off = (size_t)lo * 2 * C::NP64;
+        ZK_CHECK(hipMemcpyAsync(b + off, points + off, (size_t)(hi - lo) * 2 * C::NP64 * 8, hipMemcpyHostToDevice, st2));
+        ZK_CHECK(hipEventRecord(dev.split_event(3 * h + 1), st2));
         ready_pt[h].store(1, std::memory_order_release);
       }
     });
@@ -1727,11 +1812,14 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
       // (only a single-pass shape is split, so the first group has the splits of the copies)
       ZK_REQUIRE(sg.NS == NS, "msm: split pipeline shape mismatch (internal)");
       for (int h = 0; h < NS; h++) {
-        pass.wait_sc.push_back(dev.split_event(2 * h));
-        pass.wait_pt.push_back(dev.split_event(2 * h + 1));
+        pass.wait_sc.push_back(dev.split_event(3 * h));
+        pass.wait_pt.push_back(dev.split_event(3 * h + 1));
+        pass.sorted_ev.push_back(dev.split_event(3 * h + 2));
       }
       pass.ready_sc = ready_sc;
       pass.ready_pt = ready_pt;
+      pass.pts_ref = pts_ref;
+      if (NS > 1) pass.sst = dev.aux2_stream();
     }
     inputs_on_aux = false;
     pass.launch();
@@ -1825,6 +1913,16 @@ void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool
     for (auto &t : th) t.join();
     zkh::xyzz_set_inf(acc);
     for (int k = 0; k < G; k++) zkh::xyzz_add(acc, acc, part[k]);
+  } else if (G == 1) {  // a one-entry set pins the host-buffer MSM to that device
+    int prev = 0;
+    ZK_CHECK(hipGetDevice(&prev));
+    ZK_CHECK(hipSetDevice(set[0]));
+    {
+      Device &dev = current_device();
+      std::lock_guard<std::mutex> lock(dev.mu);
+      msm_xyzz<C>(dev, n, scalars, nl, points, host_inputs, mont, window, acc);
+    }
+    ZK_CHECK(hipSetDevice(prev));
   } else {
     Device &dev = current_device();
     std::lock_guard<std::mutex> lock(dev.mu);

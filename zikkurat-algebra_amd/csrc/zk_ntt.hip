@@ -817,10 +817,29 @@ void ntt_release(Device &dev) {
 void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64_t *dst, bool host_io,
          bool inverse) {
   ZK_REQUIRE(m >= 0 && m <= 30, "ntt: log2 size out of range (0..30)");
-  const std::vector<int> set = host_io && m >= 16 ? device_set() : std::vector<int>();
+  std::vector<int> set = host_io && m >= 16 ? device_set() : std::vector<int>();
+  int cur = 0;
+  ZK_CHECK(hipGetDevice(&cur));
+  if (!set.empty()) {
+    // compute on the calling thread's device when the set lists it (one thread or rank per GPU
+    // keeps its transforms on its own GPU), else on the first listed device
+    const auto it = std::find(set.begin(), set.end(), cur);
+    if (it != set.end()) std::rotate(set.begin(), it, set.end());
+  }
+  if (set.size() == 1 && set[0] != cur) {  // a one-entry set pins the transform to that device
+    ZK_CHECK(hipSetDevice(set[0]));
+    {
+      Device &dev = current_device();
+      std::lock_guard<std::mutex> lock(dev.mu);
+      if (curve == 0) ntt_run<CfgBN>(dev, curve, m, gen_mont, src, dst, host_io, inverse);
+      else ntt_run<CfgBLS>(dev, curve, m, gen_mont, src, dst, host_io, inverse);
+    }
+    ZK_CHECK(hipSetDevice(cur));
+    return;
+  }
   if (set.size() > 1) {
-    // compute on the first listed device, host I/O spread over every listed one; the contexts
-    // are locked in uid order (concurrent calls with other sets cannot deadlock)
+    // compute on the first device of the (rotated) set, host I/O spread over every listed one;
+    // the contexts are locked in uid order (concurrent calls with other sets cannot deadlock)
     const int G = (int)set.size();
     std::vector<Device *> ctx(G);
     for (int k = 0; k < G; k++) {

@@ -75,6 +75,11 @@ hipStream_t Device::aux_stream() {
   return aux;
 }
 
+hipStream_t Device::aux2_stream() {
+  if (!aux2) ZK_CHECK(hipStreamCreateWithFlags(&aux2, hipStreamNonBlocking));
+  return aux2;
+}
+
 hipEvent_t Device::split_event(int h) {
   while ((int)split_ev.size() <= h) {
     hipEvent_t e;

@@ -97,6 +97,10 @@ struct Device {
   hipStream_t aux = nullptr;
   hipEvent_t aux_ev = nullptr;
   hipStream_t aux_stream();
+  // third stream: the bucket sorts of a split host-input MSM run on it beside the previous
+  // split's accumulation (created on first use)
+  hipStream_t aux2 = nullptr;
+  hipStream_t aux2_stream();
   std::vector<hipEvent_t> split_ev;  // per point split of a host-input MSM (split_event)
   hipEvent_t split_event(int h);
   void release_memory();         // arena + pinned staging (caller holds mu, stream idle)

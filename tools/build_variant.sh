@@ -25,6 +25,6 @@ for o in "$PKG"/build/*.o; do
   case " $UNITS " in *" $b "*) ;; *) OBJS="$OBJS $o" ;; esac
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,-Bsymbolic -Wl,--no-undefined $OBJS \
-  -o "$OUT/libzkalgebra_gpu.so" -lpthread
+  -o "$OUT/libzkalgebra_gpu.so" -lpthread -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "$FLAGS" > "$OUT/FLAGS"
 echo "built $OUT/libzkalgebra_gpu.so ($FLAGS)"

@@ -361,6 +361,27 @@ __device__ __forceinline__ void xyzz_add_red(Xyzz<F> &acc, const Xyzz<F> &b) {
   else xyzz_add(acc, b);
 }
 
+// XYZZ storage: 4 consecutive field elements, F::SN u32 words each (shared by the MSM and the
+// group FFT kernels)
+template <class F>
+__device__ __forceinline__ void xyzz_store(uint32_t *p, const Xyzz<F> &a) {
+  fe_store_u(p + 0 * F::SN, a.X);
+  fe_store_u(p + 1 * F::SN, a.Y);
+  fe_store_u(p + 2 * F::SN, a.ZZ);
+  fe_store_u(p + 3 * F::SN, a.ZZZ);
+}
+template <class F>
+__device__ __forceinline__ void xyzz_load(Xyzz<F> &a, const uint32_t *p) {
+  fe_load_u(a.X, p + 0 * F::SN);
+  fe_load_u(a.Y, p + 1 * F::SN);
+  fe_load_u(a.ZZ, p + 2 * F::SN);
+  fe_load_u(a.ZZZ, p + 3 * F::SN);
+}
+template <class F>
+constexpr int xyzz_words() { return 4 * F::SN; }
+template <class F>
+constexpr int aff_words() { return 2 * F::SN; }
+
 // Affine points on the device are kept in INTERNAL form (converted once per call by
 // k_points_int): 2 x SN u32 words; the reference's all-0xFF infinity sentinel becomes a
 // first word of 0xFFFFFFFF (never a valid limb).  Returns false for infinity.

@@ -38,33 +38,13 @@
 #include <thread>
 #include <vector>
 #include "zk_curve.hpp"
+#include "zk_quad.hpp"
 #include "zk_host.hpp"
 #include "zk_runtime.hpp"
 #include "zk_msm.hpp"
 #include "zk_ntt.hpp"
 
 namespace zk {
-
-// ---------------------------------------------------------------------------
-// XYZZ storage: 4 consecutive field elements, F::N u32 words each.
-template <class F>
-__device__ __forceinline__ void xyzz_store(uint32_t *p, const Xyzz<F> &a) {
-  fe_store_u(p + 0 * F::SN, a.X);
-  fe_store_u(p + 1 * F::SN, a.Y);
-  fe_store_u(p + 2 * F::SN, a.ZZ);
-  fe_store_u(p + 3 * F::SN, a.ZZZ);
-}
-template <class F>
-__device__ __forceinline__ void xyzz_load(Xyzz<F> &a, const uint32_t *p) {
-  fe_load_u(a.X, p + 0 * F::SN);
-  fe_load_u(a.Y, p + 1 * F::SN);
-  fe_load_u(a.ZZ, p + 2 * F::SN);
-  fe_load_u(a.ZZZ, p + 3 * F::SN);
-}
-template <class F>
-constexpr int xyzz_words() { return 4 * F::SN; }
-template <class F>
-constexpr int aff_words() { return 2 * F::SN; }
 
 // 0. affine points: reference form -> internal form (once per call).  The block's 256 points
 // are one contiguous span on both sides (96 / 64 B in, 128 / 96 B out): they are staged through
@@ -709,6 +689,76 @@ __global__ void __launch_bounds__(BS) k_stitch_blk(const uint32_t *__restrict__ 
   if (touches_end) okeys[2 * blk + 1] = touches_start ? nb : item_key;
 }
 
+// 5c''. quad-cooperative form of k_stitch_blk (G1, level 0): 64 compacted items per 256-thread
+//      block, one QUAD per item, so every Hillis-Steele step is one xyzz_add_quad (5 product
+//      latencies) instead of a one-lane full add (14): the stitch is latency-bound (a few steps
+//      per block at any size), and at small inputs it was the largest phase (BLS12-381 2^10: 109 of
+//      the stitch's 130 us in k_stitch_blk, profiles/r04d_*).  Same item / slot contract as
+//      k_stitch_blk with BS = 64.
+#ifndef ZK_STITCH_QUAD
+#define ZK_STITCH_QUAD 1
+#endif
+constexpr int STITCH_QBS = 64;  // items per block of k_stitch_blk_q
+template <class C>
+__global__ void __launch_bounds__(256) k_stitch_blk_q(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ idx,
+                                                      const uint32_t *__restrict__ vals,
+                                                      const uint32_t *__restrict__ count, uint32_t nb,
+                                                      uint32_t *__restrict__ buckets, uint32_t *__restrict__ okeys,
+                                                      uint32_t *__restrict__ ovals, uint32_t nout) {
+  using F = typename C::Fp;
+  constexpr int XW = xyzz_words<F>();
+  constexpr uint32_t BSQ = STITCH_QBS;
+  __shared__ uint4 item_lds4[BSQ * XW / 4];  // [BSQ][XW] partial sums (16 KB: several blocks per CU)
+  __shared__ uint32_t skey[BSQ];
+  uint32_t *lv = reinterpret_cast<uint32_t *>(item_lds4);
+  uint32_t *const park = nullptr;  // doubling fallback straight from the accumulator
+  const uint32_t M = *count;
+  const uint32_t tq = threadIdx.x >> 2, q = threadIdx.x & 3, blk = blockIdx.x;
+  const uint32_t base = blk * BSQ;
+  if (base >= M) {  // no items: clear this block's output slots
+    if (threadIdx.x < 2 && 2 * blk + threadIdx.x < nout) okeys[2 * blk + threadIdx.x] = nb;
+    return;
+  }
+  const uint32_t nv = min(BSQ, M - base);  // valid quads
+  const uint32_t j = base + tq;
+  const bool valid = tq < nv;  // quad-uniform
+  const uint32_t key = valid ? keys[j] : 0xffffffffu;
+  if (q == 0) skey[tq] = key;
+  Xyzz<F> acc;
+  if (valid) xyzz_load(acc, vals + (size_t)idx[j] * XW);
+  else xyzz_set_inf(acc);
+  __syncthreads();
+  for (uint32_t d = 1; d < nv; d <<= 1) {
+    const bool need = valid && tq >= d && skey[tq - d] == key;
+    if (!__syncthreads_or(need)) break;
+    xyzz_store_quad(lv + (size_t)tq * XW, acc, (int)q);
+    __syncthreads();
+    if (need) {
+      Xyzz<F> o;
+      xyzz_load(o, lv + (size_t)(tq - d) * XW);
+      xyzz_add_quad(acc, o, park);
+    }
+    __syncthreads();
+  }
+  if (!valid) return;
+  const bool seg_last = tq == nv - 1 || skey[tq + 1] != key;
+  if (!seg_last) return;
+  const bool touches_start = skey[0] == key;
+  const bool touches_end = tq == nv - 1;
+  const bool cont_in = touches_start && base > 0 && keys[base - 1] == key;
+  const bool cont_out = touches_end && base + nv < M && keys[base + nv] == key;
+  if (!cont_in && !cont_out) {
+    xyzz_store_quad(buckets + (size_t)key * XW, acc, (int)q);
+  } else {
+    xyzz_store_quad(ovals + (size_t)(touches_start ? 2 * blk : 2 * blk + 1) * XW, acc, (int)q);
+  }
+  if (q == 0) {
+    const uint32_t item_key = (cont_in || cont_out) ? key : nb;
+    if (touches_start) okeys[2 * blk] = item_key;
+    if (touches_end) okeys[2 * blk + 1] = touches_start ? nb : item_key;
+  }
+}
+
 // 5c'. block stitch level straight on the item SLOTS (no global compaction): block b takes
 //      slots [b BS, (b+1) BS), packs its valid items (key < nb) into LDS in slot order
 //      (wavefront ballots + a block prefix), and sums them per key by a segmented TREE
@@ -917,12 +967,16 @@ __global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ bucke
   }
 }
 
+#ifndef ZK_YSUM_QUAD_FOLD
+#define ZK_YSUM_QUAD_FOLD 1  // k_ysum2's block fold with quad-cooperative additions (G1)
+#endif
 // 6'. k_ysum2: block-level form of k_ysum, used when each region fills whole 256-lane
 //     blocks (every shape from c = 12 up at the default QY).  Segment s of a block owns the
 //     STRIDED lanes {s, s + S, s + 2S, ...} (S = 256 / G segments per block), so the fold
 //     pairs lane t with lane t + h (h = 128 ... S): the upper half parks its partial in LDS
 //     and drops out, the lower half adds it -- whole wavefronts leave the fold as h
 //     shrinks, where k_ysum's in-wavefront fold keeps every lane adding at every step.
+//     For G1 the fold's additions are quad-cooperative (xyzz_add_quad, 64 per round).
 //     The next bucket's emptiness test (and, with PF, its data) is loaded one iteration
 //     ahead: at one or two waves per SIMD nothing else hides those latencies.
 template <class C, bool PF>
@@ -932,8 +986,13 @@ __global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buck
                                                SegRegion r0, SegRegion r1, uint32_t *__restrict__ Y) {
   using F = typename C::Fp;
   constexpr int XW = xyzz_words<F>();
-  __shared__ uint4 park4[128 * XW / 4];
+  // G1: the fold runs quad-cooperatively (2 x 64 KB of LDS for BLS12-381: the parked sums and
+  // xyzz_add_quad's per-lane doubling fallback); Fp2 points keep the one-lane fold (LDS)
+  constexpr bool QUAD_FOLD = ZK_YSUM_QUAD_FOLD && XW <= 64;
+  __shared__ uint4 park4[(QUAD_FOLD ? 256 : 128) * XW / 4];
+  __shared__ uint4 fold4[QUAD_FOLD ? 256 * XW / 4 : 1];
   uint32_t *park = reinterpret_cast<uint32_t *>(park4);
+  uint32_t *fold = reinterpret_cast<uint32_t *>(fold4);
   const int l1 = c - 1 - l0;
   const int NY = (1 << l0) + (1 << l1);
   const int nb0 = r0.count * r0.G / 256, nb1 = r1.count * r1.G / 256;  // blocks per window and region
@@ -975,118 +1034,49 @@ __global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buck
       xyzz_add_red(acc, cur);
     }
   }
-  for (int h = 128; h >= S; h >>= 1) {
-    if (t >= h && t < 2 * h) xyzz_store(park + (size_t)(t - h) * XW, acc);
+  if constexpr (QUAD_FOLD) {
+    // quad-cooperative fold: every lane parks its sum; level h adds slot a + h into slot a (a < h)
+    // with 4 lanes per addition (xyzz_add_quad: 5 product latencies instead of 14), 64 additions
+    // per round.  Slots read in a round (a, a + h) are never written in it (writes go to a < h).
+    xyzz_store(fold + (size_t)t * XW, acc);
     __syncthreads();
-    if (t < h) {
-      Xyzz<F> o;
-      xyzz_load(o, park + (size_t)t * XW);
-      xyzz_add_red(acc, o);
+    const int q = t >> 2;
+    for (int h = 128; h >= S; h >>= 1) {
+      for (int base = 0; base < h; base += 64) {
+        const int a = base + q;
+        Xyzz<F> x;
+        if (a < h) {  // quad-uniform
+          Xyzz<F> o;
+          xyzz_load(x, fold + (size_t)a * XW);
+          xyzz_load(o, fold + (size_t)(a + h) * XW);
+          xyzz_add_quad(x, o, park + (size_t)t * XW);
+        }
+        __syncthreads();
+        if (a < h && (t & 3) == 0) xyzz_store(fold + (size_t)a * XW, x);
+      }
+      __syncthreads();
     }
-    __syncthreads();
-  }
-  if (t < S) {
-    const int y = hiY ? (1 << l0) + seg : seg;
-    xyzz_store(Y + ((size_t)w * NY + y) * XW, acc);
-  }
-}
-
-// Quad-cooperative XYZZ addition (add-2008-s) for latency-bound phases: the 4 lanes of an
-// aligned quad hold acc and b REPLICATED and split the 14 products by dependency level
-//   L1: U1 = X1 ZZ2, U2 = X2 ZZ1, S1 = Y1 ZZZ2, S2 = Y2 ZZZ1 | ZZ1 ZZ2, ZZZ1 ZZZ2   (2 deep)
-//   L2: PP = P^2, RR = R^2                                                             (1)
-//   L3: PPP = P PP, Q = U1 PP, ZZ3 = (ZZ1 ZZ2) PP                                      (1)
-//   L4: R (Q - X3), S1 PPP, ZZZ3 = (ZZZ1 ZZZ2) PPP                                     (1)
-// with quad broadcasts in between: 5 product latencies instead of 14.  Every lane executes
-// the same instruction stream (operands picked by selects, not branches); the result is
-// replicated again.  Special cases are decided on replicated values, so quads never split.
-template <class F>
-__device__ __forceinline__ void fe_sel4(Fe<F> &r, const Fe<F> &v0, const Fe<F> &v1, const Fe<F> &v2,
-                                        const Fe<F> &v3, int q) {
-  // explicit masks: a ternary chain here is lowered to an indexed private array (scratch)
-  const uint32_t k0 = 0u - (uint32_t)(q == 0), k1 = 0u - (uint32_t)(q == 1);
-  const uint32_t k2 = 0u - (uint32_t)(q == 2), k3 = 0u - (uint32_t)(q == 3);
-#pragma unroll
-  for (int i = 0; i < F::N; i++) r.v[i] = (v0.v[i] & k0) | (v1.v[i] & k1) | (v2.v[i] & k2) | (v3.v[i] & k3);
-}
-// quad broadcast from lane SRC of the quad: DPP quad_perm [SRC,SRC,SRC,SRC] (one VALU move
-// per word, no LDS round trip)
-template <int SRC, class F>
-__device__ __forceinline__ void fe_bcast(Fe<F> &r, const Fe<F> &v) {
-#pragma unroll
-  for (int i = 0; i < F::N; i++)
-    r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v[i], SRC * 0x55, 0xf, 0xf, false);
-}
-template <class F>
-__device__ __forceinline__ void xyzz_add_quad(Xyzz<F> &acc, const Xyzz<F> &b, uint32_t *__restrict__ park) {
-  if (xyzz_is_inf(b)) return;
-  if (xyzz_is_inf(acc)) { acc = b; return; }
-  const int q = (int)(threadIdx.x & 3);
-  xyzz_store(park, acc);  // only the rare doubling branch reads it back
-  Fe<F> x, y, m1, m2;
-  fe_sel4(x, acc.X, b.X, acc.Y, b.Y, q);
-  fe_sel4(y, b.ZZ, acc.ZZ, b.ZZZ, acc.ZZZ, q);
-  fe_mul(m1, x, y);  // q: U1, U2, S1, S2 (kept in the producing lane)
-  fe_sel4(x, acc.ZZ, acc.ZZZ, acc.ZZ, acc.ZZZ, q);
-  fe_sel4(y, b.ZZ, b.ZZZ, b.ZZ, b.ZZZ, q);
-  fe_mul(m2, x, y);  // q0: ZZ1 ZZ2, q1: ZZZ1 ZZZ2
-  Fe<F> P, R;
-  {
-    Fe<F> u, v;
-    fe_bcast<0>(u, m1);
-    fe_bcast<1>(v, m1);
-    fe_sub(P, v, u);  // U2 - U1
-    fe_bcast<2>(u, m1);
-    fe_bcast<3>(v, m1);
-    fe_sub(R, v, u);  // S2 - S1
-  }
-  Fe<F> PP, RR;
-  fe_sel4(x, P, R, P, R, q);
-  fe_sqr(y, x);  // q0: PP, q1: RR
-  fe_bcast<0>(PP, y);
-  fe_bcast<1>(RR, y);
-  if (fe_is_zero(PP)) {  // P == 0 (replicated: the whole quad agrees)
-    if (fe_is_zero(RR)) {
-      Xyzz<F> a0, d;
-      xyzz_load(a0, park);
-      xyzz_dbl(d, a0);
-      acc = d;
-    } else {
-      xyzz_set_inf(acc);
+    if (t < S) {
+      xyzz_load(acc, fold + (size_t)t * XW);
+      const int y = hiY ? (1 << l0) + seg : seg;
+      xyzz_store(Y + ((size_t)w * NY + y) * XW, acc);
     }
-    return;
+  } else {
+    for (int h = 128; h >= S; h >>= 1) {
+      if (t >= h && t < 2 * h) xyzz_store(park + (size_t)(t - h) * XW, acc);
+      __syncthreads();
+      if (t < h) {
+        Xyzz<F> o;
+        xyzz_load(o, park + (size_t)t * XW);
+        xyzz_add_red(acc, o);
+      }
+      __syncthreads();
+    }
+    if (t < S) {
+      const int y = hiY ? (1 << l0) + seg : seg;
+      xyzz_store(Y + ((size_t)w * NY + y) * XW, acc);
+    }
   }
-  Fe<F> PPP, Q, ZZ3;
-  {
-    Fe<F> u1, zza;
-    fe_bcast<0>(u1, m1);
-    fe_bcast<0>(zza, m2);
-    fe_sel4(x, P, u1, zza, P, q);
-    fe_mul(y, x, PP);  // q0: PPP, q1: Q, q2: ZZ3
-    fe_bcast<0>(PPP, y);
-    fe_bcast<1>(Q, y);
-    fe_bcast<2>(ZZ3, y);
-  }
-  Fe<F> X3, t;
-  fe_sub(t, RR, PPP);
-  fe_sub(t, t, Q);
-  fe_sub(X3, t, Q);  // X3 = RR - PPP - 2Q
-  fe_sub(t, Q, X3);
-  {
-    Fe<F> s1, zzza;
-    fe_bcast<2>(s1, m1);
-    fe_bcast<1>(zzza, m2);
-    fe_sel4(x, R, s1, zzza, R, q);
-    fe_sel4(y, t, PPP, PPP, t, q);
-  }
-  fe_mul(m1, x, y);  // q0: R (Q - X3), q1: S1 PPP, q2: ZZZ3
-  Fe<F> a0, a1;
-  fe_bcast<0>(a0, m1);
-  fe_bcast<1>(a1, m1);
-  fe_sub(acc.Y, a0, a1);
-  fe_bcast<2>(acc.ZZZ, m1);
-  acc.X = X3;
-  acc.ZZ = ZZ3;
 }
 
 // 7. weighted Y sums by bit jobs: one 256-thread block per (window, job) = 64 quad lanes
@@ -1295,6 +1285,9 @@ inline int MsmShape::split_ch(int h) const {
 // buffer stays at 64 KB
 template <class F>
 constexpr int stitch_bs() { return xyzz_words<F>() > 64 ? 128 : 256; }
+// items per block of the level-0 stitch (the quad-cooperative kernel's 64 for G1)
+template <class F>
+constexpr int stitch_bs0() { return (ZK_STITCH_QUAD && xyzz_words<F>() <= 64) ? STITCH_QBS : stitch_bs<F>(); }
 
 static size_t stitch_slots0(const MsmShape &s) {  // item slots of the largest split's accumulation
   size_t m = 0;
@@ -1327,7 +1320,7 @@ static size_t group_bytes(const MsmShape &s) {
   const size_t xw = xyzz_words<F>() * 4;  // bytes per XYZZ
   const size_t nb = (size_t)s.W * s.B;
   const size_t maxent = (size_t)s.W * s.n;
-  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s, stitch_bs<F>());
+  const size_t ns0 = stitch_slots0(s), ns1 = stitch_slots1(s, stitch_bs0<F>());
   size_t cub = 0, cub2 = 0;
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(s.nmat() + 1)));
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)ns0));
@@ -1453,7 +1446,7 @@ struct GroupPass {
     offsets = dev.arena.take<uint32_t>((size_t)s.NS * (nb + 1));  // split h: offsets + h (nb + 1)
     if (s.NS > 1) filled = dev.arena.take<uint8_t>(nb);
     ns0 = stitch_slots0(s);
-    ns1 = stitch_slots1(s, STITCH_BS);
+    ns1 = stitch_slots1(s, stitch_bs0<F>());
     ikeys0 = dev.arena.take<uint32_t>(ns0);
     ivals0 = dev.arena.take<uint32_t>(ns0 * xw);
     ckeys = dev.arena.take<uint32_t>(ns0);
@@ -1537,10 +1530,12 @@ struct GroupPass {
                        pts_ref + (size_t)lo * 2 * C::NP64, hi - lo, const_cast<uint32_t *>(pts_int) + (size_t)lo * aff_words<F>());
     ZK_CHECK(hipGetLastError());
   }
+  int ch0 = 0;  // chunk length of the accumulation whose items the stitch is summing
   void accumulate(int sp) {
     if (sp == 0) timer_begin(dev, timer_slot, st);
     const size_t npts = (size_t)s.split_lo(sp + 1) - (size_t)s.split_lo(sp);
     const int CH = s.split_ch(sp);
+    ch0 = CH;
     const size_t nsl = 2 * (((size_t)s.W * npts + CH - 1) / CH);  // <= ns0
     // upper bound on the chunk count; threads past the range's end only clear their item slots
     hipLaunchKernelGGL(k_accum<C>, dim3(div_up(nsl / 2, 256)), dim3(256), 0, st, pts_int, list,
@@ -1565,9 +1560,17 @@ struct GroupPass {
   // every item completed at this level
   int level = 0;
   bool stitch_level() {
-    const bool final_level = slots <= (size_t)STITCH_BS;  // all items fit one block: everything completes
-    const size_t nout = final_level ? 2 : 2 * ((slots + STITCH_BS - 1) / STITCH_BS);
-    if (ZK_STITCH_RAW && level++ > 0) {  // one kernel per level, straight on the slots
+    const bool raw = ZK_STITCH_RAW && level++ > 0;
+    // the quad-cooperative level-0 kernel wins where its blocks fit about one round on the chip:
+    // few item slots (small inputs) or long chunks (CH 64: runs mostly complete inside a lane or
+    // merged in-wave, so few items survive compaction); with many items (2^16-2^18, CH 10-32)
+    // the one-lane kernel's 4x fewer blocks win (BLS12-381 2^16: 0.196 vs 0.220 ms stitch,
+    // 2^10: 0.150 vs 0.094, 2^20: 0.052 vs 0.041; profiles/r04f_*)
+    const bool quad0 = stitch_bs0<F>() == STITCH_QBS && (ns0 <= 65536 || ch0 >= 64);
+    const int bs = raw ? STITCH_BS : (quad0 ? STITCH_QBS : STITCH_BS);  // items per block at this level
+    const bool final_level = slots <= (size_t)bs;  // all items fit one block: everything completes
+    const size_t nout = final_level ? 2 : 2 * ((slots + bs - 1) / bs);
+    if (raw) {  // one kernel per level, straight on the slots
       hipLaunchKernelGGL((k_stitch_raw<C, STITCH_BS>), dim3((unsigned)((slots + STITCH_BS - 1) / STITCH_BS)),
                          dim3(STITCH_BS), 0, st, inK, inV, (uint32_t)slots, (uint32_t)nb, final_level ? 1 : 0,
                          buckets, outK, outV);
@@ -1581,9 +1584,18 @@ struct GroupPass {
       hipLaunchKernelGGL(k_item_index, dim3(div_up(slots, 256)), dim3(256), 0, st, inK, flags, pos, (uint32_t)slots,
                          ckeys, cidx, ccount);
       ZK_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((k_stitch_blk<C, STITCH_BS>), dim3((unsigned)(nout / 2)), dim3(STITCH_BS), 0, st, ckeys,
-                         cidx, inV, ccount, (uint32_t)nb, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV,
-                         (uint32_t)nout);
+      bool launched = false;
+      if constexpr (stitch_bs0<F>() == STITCH_QBS) {
+        if (quad0) {
+          hipLaunchKernelGGL(k_stitch_blk_q<C>, dim3((unsigned)(nout / 2)), dim3(256), 0, st, ckeys, cidx, inV, ccount,
+                             (uint32_t)nb, buckets, outK, outV, (uint32_t)nout);
+          launched = true;
+        }
+      }
+      if (!launched)
+        hipLaunchKernelGGL((k_stitch_blk<C, STITCH_BS>), dim3((unsigned)(nout / 2)), dim3(STITCH_BS), 0, st, ckeys,
+                           cidx, inV, ccount, (uint32_t)nb, (uint32_t)s.W, (uint32_t)s.B, buckets, outK, outV,
+                           (uint32_t)nout);
       ZK_CHECK(hipGetLastError());
     }
     inK = outK; inV = outV; slots = nout;

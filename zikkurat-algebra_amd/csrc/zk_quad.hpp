@@ -1,0 +1,162 @@
+// zk_quad.hpp -- quad-cooperative XYZZ point operations for latency-bound phases (the MSM's
+// Y-sum fold and job sums, the group FFT's scalar multiplications): the 4 lanes of an aligned
+// quad hold the operands REPLICATED and split one point operation's products by dependency
+// level, exchanging results with DPP quad broadcasts, so an operation costs its dependency
+// depth in product latencies instead of its product count.
+#pragma once
+#include "zk_curve.hpp"
+
+namespace zk {
+
+// Quad-cooperative XYZZ addition (add-2008-s) for latency-bound phases: the 4 lanes of an
+// aligned quad hold acc and b REPLICATED and split the 14 products by dependency level
+//   L1: U1 = X1 ZZ2, U2 = X2 ZZ1, S1 = Y1 ZZZ2, S2 = Y2 ZZZ1 | ZZ1 ZZ2, ZZZ1 ZZZ2   (2 deep)
+//   L2: PP = P^2, RR = R^2                                                             (1)
+//   L3: PPP = P PP, Q = U1 PP, ZZ3 = (ZZ1 ZZ2) PP                                      (1)
+//   L4: R (Q - X3), S1 PPP, ZZZ3 = (ZZZ1 ZZZ2) PPP                                     (1)
+// with quad broadcasts in between: 5 product latencies instead of 14.  Every lane executes
+// the same instruction stream (operands picked by selects, not branches); the result is
+// replicated again.  Special cases are decided on replicated values, so quads never split.
+template <class F>
+__device__ __forceinline__ void fe_sel4(Fe<F> &r, const Fe<F> &v0, const Fe<F> &v1, const Fe<F> &v2,
+                                        const Fe<F> &v3, int q) {
+  // explicit masks: a ternary chain here is lowered to an indexed private array (scratch)
+  const uint32_t k0 = 0u - (uint32_t)(q == 0), k1 = 0u - (uint32_t)(q == 1);
+  const uint32_t k2 = 0u - (uint32_t)(q == 2), k3 = 0u - (uint32_t)(q == 3);
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = (v0.v[i] & k0) | (v1.v[i] & k1) | (v2.v[i] & k2) | (v3.v[i] & k3);
+}
+// quad broadcast from lane SRC of the quad: DPP quad_perm [SRC,SRC,SRC,SRC] (one VALU move
+// per word, no LDS round trip)
+template <int SRC, class F>
+__device__ __forceinline__ void fe_bcast(Fe<F> &r, const Fe<F> &v) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++)
+    r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v[i], SRC * 0x55, 0xf, 0xf, false);
+}
+template <class F>
+__device__ __forceinline__ void xyzz_add_quad(Xyzz<F> &acc, const Xyzz<F> &b, uint32_t *__restrict__ park) {
+  if (xyzz_is_inf(b)) return;
+  if (xyzz_is_inf(acc)) { acc = b; return; }
+  const int q = (int)(threadIdx.x & 3);
+  if (park) xyzz_store(park, acc);  // only the rare doubling branch reads it back (nullptr: from acc)
+  Fe<F> x, y, m1, m2;
+  fe_sel4(x, acc.X, b.X, acc.Y, b.Y, q);
+  fe_sel4(y, b.ZZ, acc.ZZ, b.ZZZ, acc.ZZZ, q);
+  fe_mul(m1, x, y);  // q: U1, U2, S1, S2 (kept in the producing lane)
+  fe_sel4(x, acc.ZZ, acc.ZZZ, acc.ZZ, acc.ZZZ, q);
+  fe_sel4(y, b.ZZ, b.ZZZ, b.ZZ, b.ZZZ, q);
+  fe_mul(m2, x, y);  // q0: ZZ1 ZZ2, q1: ZZZ1 ZZZ2
+  Fe<F> P, R;
+  {
+    Fe<F> u, v;
+    fe_bcast<0>(u, m1);
+    fe_bcast<1>(v, m1);
+    fe_sub(P, v, u);  // U2 - U1
+    fe_bcast<2>(u, m1);
+    fe_bcast<3>(v, m1);
+    fe_sub(R, v, u);  // S2 - S1
+  }
+  Fe<F> PP, RR;
+  fe_sel4(x, P, R, P, R, q);
+  fe_sqr(y, x);  // q0: PP, q1: RR
+  fe_bcast<0>(PP, y);
+  fe_bcast<1>(RR, y);
+  if (fe_is_zero(PP)) {  // P == 0 (replicated: the whole quad agrees)
+    if (fe_is_zero(RR)) {
+      Xyzz<F> a0, d;
+      if (park) xyzz_load(a0, park);
+      else a0 = acc;  // acc is still unmodified here
+      xyzz_dbl(d, a0);
+      acc = d;
+    } else {
+      xyzz_set_inf(acc);
+    }
+    return;
+  }
+  Fe<F> PPP, Q, ZZ3;
+  {
+    Fe<F> u1, zza;
+    fe_bcast<0>(u1, m1);
+    fe_bcast<0>(zza, m2);
+    fe_sel4(x, P, u1, zza, P, q);
+    fe_mul(y, x, PP);  // q0: PPP, q1: Q, q2: ZZ3
+    fe_bcast<0>(PPP, y);
+    fe_bcast<1>(Q, y);
+    fe_bcast<2>(ZZ3, y);
+  }
+  Fe<F> X3, t;
+  fe_sub(t, RR, PPP);
+  fe_sub(t, t, Q);
+  fe_sub(X3, t, Q);  // X3 = RR - PPP - 2Q
+  fe_sub(t, Q, X3);
+  {
+    Fe<F> s1, zzza;
+    fe_bcast<2>(s1, m1);
+    fe_bcast<1>(zzza, m2);
+    fe_sel4(x, R, s1, zzza, R, q);
+    fe_sel4(y, t, PPP, PPP, t, q);
+  }
+  fe_mul(m1, x, y);  // q0: R (Q - X3), q1: S1 PPP, q2: ZZZ3
+  Fe<F> a0, a1;
+  fe_bcast<0>(a0, m1);
+  fe_bcast<1>(a1, m1);
+  fe_sub(acc.Y, a0, a1);
+  fe_bcast<2>(acc.ZZZ, m1);
+  acc.X = X3;
+  acc.ZZ = ZZ3;
+}
+
+// lane q of the quad stores coordinate q of a replicated point
+template <class F>
+__device__ __forceinline__ void xyzz_store_quad(uint32_t *__restrict__ p, const Xyzz<F> &a, int q) {
+  Fe<F> c;
+  fe_sel4(c, a.X, a.Y, a.ZZ, a.ZZZ, q);
+  fe_store_u(p + q * F::SN, c);
+}
+
+// Quad-cooperative doubling (dbl-2008-s-1, a = 0): 9 products in 3 dependency levels
+//   L1: V = U^2 (U = 2Y), X^2
+//   L2: W = U V, S = X V, M^2 (M = 3 X^2), ZZ3 = V ZZ
+//   L3: M (S - X3), W Y, ZZZ3 = W ZZZ
+// Inputs / outputs replicated over the quad.  Infinity stays infinity (no 2-torsion on the G1
+// curves: their group orders are odd).
+template <class F>
+__device__ __forceinline__ void xyzz_dbl_quad(Xyzz<F> &acc) {
+  if (xyzz_is_inf(acc)) return;
+  const int q = (int)(threadIdx.x & 3);
+  Fe<F> U, x, y, m;
+  fe_add(U, acc.Y, acc.Y);
+  fe_sel4(x, U, acc.X, U, acc.X, q);
+  fe_sqr(m, x);  // q0: V, q1: X^2
+  Fe<F> V, M;
+  fe_bcast<0>(V, m);
+  {
+    Fe<F> x2;
+    fe_bcast<1>(x2, m);
+    fe_mul3(M, x2);
+  }
+  fe_sel4(x, U, acc.X, M, V, q);
+  fe_sel4(y, V, V, M, acc.ZZ, q);
+  fe_mul(m, x, y);  // q0: W, q1: S, q2: M^2, q3: ZZ3
+  Fe<F> W, S, MM, ZZ3, X3, t;
+  fe_bcast<0>(W, m);
+  fe_bcast<1>(S, m);
+  fe_bcast<2>(MM, m);
+  fe_bcast<3>(ZZ3, m);
+  fe_sub(t, MM, S);
+  fe_sub(X3, t, S);  // X3 = M^2 - 2S
+  fe_sub(t, S, X3);
+  fe_sel4(x, M, W, W, M, q);
+  fe_sel4(y, t, acc.Y, acc.ZZZ, t, q);
+  fe_mul(m, x, y);  // q0: M (S - X3), q1: W Y, q2: ZZZ3
+  Fe<F> a0, a1;
+  fe_bcast<0>(a0, m);
+  fe_bcast<1>(a1, m);
+  fe_sub(acc.Y, a0, a1);
+  fe_bcast<2>(acc.ZZZ, m);
+  acc.X = X3;
+  acc.ZZ = ZZ3;
+}
+
+}  // namespace zk

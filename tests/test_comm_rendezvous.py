@@ -1,0 +1,86 @@
+"""The multi-GPU bench's rendezvous on the CPU: sharded.LibComm hands the RCCL unique id from
+rank 0 to the other ranks through a file (no torch, no TCP store), then every rank calls
+zkg_comm_init with it.  Here the library's zkg_comm_* entry points are replaced by a recording
+stand-in (the real ones need a GPU; tests/test_gpu_comm.py runs them on the GPU box), so the test
+checks exactly the Python protocol bench.py --gpus N uses: one id per launch, seen by every rank,
+the file removed afterwards, and launches with different keys kept apart."""
+import ctypes
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class _FakeLib:
+    """stand-in for the library's zkg_comm_*: init is collective like ncclCommInitRank (it returns
+    only once every rank of the launch has called it), so rank 0 may then remove the id file"""
+
+    def __init__(self, key, rdir):
+        self.key, self.rdir = key, rdir
+        self.got = None
+
+    def zkg_comm_unique_id(self, buf):
+        ctypes.memmove(buf, os.urandom(128), 128)
+        return 0
+
+    def zkg_comm_init(self, rank, world, buf):
+        self.got = (rank, world, bytes(buf.raw[:128]))
+        open(os.path.join(self.rdir, f"joined_{self.key}_{rank}"), "w").close()
+        t0 = time.time()
+        while sum(os.path.exists(os.path.join(self.rdir, f"joined_{self.key}_{r}")) for r in range(world)) < world:
+            if time.time() - t0 > 60:
+                return -1
+            time.sleep(0.01)
+        return 0
+
+    def zkg_comm_destroy(self):
+        return 0
+
+
+def _rank(rank, world, key, rdir, q):
+    sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
+    os.environ["ZKG_RDZV_KEY"] = key
+    os.environ["ZKG_RDZV_DIR"] = rdir
+    import sharded
+    fake = _FakeLib(key, rdir)
+    sharded.zk.load = lambda: fake
+    c = sharded.LibComm(rank, world, timeout=60)
+    c.close()
+    q.put((key, fake.got))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_file_rendezvous_one_id_per_launch(tmp_path, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    keys = ["launchA", "launchB"]  # two concurrent launches must not mix their ids
+    procs = [ctx.Process(target=_rank, args=(r, world, k, str(tmp_path), q)) for k in keys for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in keys:
+        got = [g for kk, g in res if kk == k]
+        assert sorted(g[0] for g in got) == list(range(world))
+        assert all(g[1] == world for g in got)
+        assert len({g[2] for g in got}) == 1  # every rank of the launch holds rank 0's id
+    ids = {g[2] for _, g in res}
+    assert len(ids) == 2
+    time.sleep(0.2)
+    assert not [f for f in os.listdir(tmp_path) if f.startswith("zkg_rdzv_")]  # removed by rank 0
+
+
+def test_rendezvous_path_default_key(monkeypatch):
+    sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
+    import sharded
+    monkeypatch.delenv("ZKG_RDZV_KEY", raising=False)
+    monkeypatch.delenv("ZKG_RDZV_DIR", raising=False)
+    monkeypatch.setenv("MASTER_PORT", "29517")
+    p = sharded.rendezvous_path()
+    assert p.endswith(f"zkg_rdzv_{os.getppid()}_29517.id")

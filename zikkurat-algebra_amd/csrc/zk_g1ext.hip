@@ -23,9 +23,7 @@
 // Scalar multiplication: fixed 4-bit windows, MSB first, 15-entry table per lane in
 // global scratch (no lane divergence on the digit: every window does one table add).
 // Outputs are normalised (Z = 1, infinity = (0:1:0)) as the reference does (:719, :785).
-#include <stdlib.h>
 #include "zk_curve.hpp"
-#include "zk_quad.hpp"
 #include "zk_host.hpp"
 #include "zk_msm.hpp"
 #include "zk_runtime.hpp"
@@ -309,145 +307,6 @@ __global__ void __launch_bounds__(256) k_fft_inv_stage(int m, int s, const uint3
   }
 }
 
-// ---- quad-cooperative group FFT stages (default): one quad (4 lanes) per scalar multiplication.
-// A stage is latency-bound -- every lane's multiplication is a chain of 255 doublings, and at 2^16
-// points a forward stage has only 2^15 of them, half a wave per SIMD with one lane each -- so the
-// quad splits every doubling (3 product latencies instead of 9, xyzz_dbl_quad) and addition (5
-// instead of 14, xyzz_add_quad) across its lanes, and the digits are signed 5-bit windows
-// (52 windows, at most 52 additions instead of 64).  Digits: K = k + sum_i 16 * 32^i, digit i =
-// bits [5i, 5i + 5) of K minus 16, in [-16, 15]; the sum telescopes back to k exactly (K < 2^260 as
-// k < 2^256 - 2^255).  The per-quad table d P, d = 1..16, lives in global scratch with lane q
-// holding coordinate q of every entry (each lane reads back only what it wrote: no cross-lane
-// memory ordering); a lookup is one coordinate per lane plus quad broadcasts.
-template <class F>
-__device__ __forceinline__ void tab_put(uint32_t *__restrict__ tab, int d, const Xyzz<F> &a, int q) {
-  Fe<F> c;
-  fe_sel4(c, a.X, a.Y, a.ZZ, a.ZZZ, q);
-  fe_store_u(tab + ((size_t)(d - 1) * 4 + q) * F::SN, c);
-}
-template <class F>
-__device__ __forceinline__ void tab_get(Xyzz<F> &a, const uint32_t *__restrict__ tab, int d, int q) {
-  Fe<F> c;
-  fe_load_u(c, tab + ((size_t)(d - 1) * 4 + q) * F::SN);
-  fe_bcast<0>(a.X, c);
-  fe_bcast<1>(a.Y, c);
-  fe_bcast<2>(a.ZZ, c);
-  fe_bcast<3>(a.ZZZ, c);
-}
-// window i (5 bits) of the 261-bit K = k + H held in 5 u64 words
-__device__ __forceinline__ uint32_t win5(const uint64_t *K, int i) {
-  const int b = 5 * i, w = b >> 6, o = b & 63;
-  uint64_t v = K[w] >> o;
-  if (o > 59 && w < 4) v |= K[w + 1] << (64 - o);
-  return (uint32_t)v & 31u;
-}
-template <class F>
-__device__ void xyzz_scl_quad(Xyzz<F> &r, const Xyzz<F> &P, const uint64_t *__restrict__ k, uint32_t *__restrict__ tab,
-                              uint32_t *__restrict__ park) {
-  const int q = (int)(threadIdx.x & 3);
-  {
-    Xyzz<F> acc = P;
-    tab_put(tab, 1, acc, q);
-    xyzz_dbl_quad(acc);
-    tab_put(tab, 2, acc, q);
-    for (int d = 3; d <= 16; d++) {
-      xyzz_add_quad(acc, P, park);
-      tab_put(tab, d, acc, q);
-    }
-  }
-  // K = k + H, H = sum_{i < 52} 16 * 32^i
-  uint64_t K[5];
-  {
-    const uint64_t H[5] = {0x0842108421084210ull, 0x1084210842108421ull, 0x2108421084210842ull,
-                           0x4210842108421084ull, 0x8ull};
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 5; j++) {
-      const uint64_t a = j < 4 ? k[j] : 0, s1 = a + H[j];
-      const uint64_t c1 = s1 < a ? 1 : 0, s2 = s1 + c;
-      K[j] = s2;
-      c = c1 | (s2 < s1 ? 1 : 0);
-    }
-  }
-  Xyzz<F> acc;
-  xyzz_set_inf(acc);
-  for (int i = 51; i >= 0; i--) {
-    if (i != 51)
-      for (int z = 0; z < 5; z++) xyzz_dbl_quad(acc);
-    const int d = (int)win5(K, i) - 16;
-    if (d) {  // quad-uniform (the scalar is replicated)
-      Xyzz<F> e;
-      tab_get(e, tab, d < 0 ? -d : d, q);
-      if (d < 0) {
-        Fe<F> ny;
-        fe_neg(ny, e.Y);
-        e.Y = ny;
-      }
-      xyzz_add_quad(acc, e, park);
-    }
-  }
-  r = acc;
-}
-
-#ifndef ZK_FFT_QUAD_WAVES
-#define ZK_FFT_QUAD_WAVES 2  // waves per SIMD the quad stages are compiled for
-#endif
-template <class C>
-__global__ void __launch_bounds__(256, ZK_FFT_QUAD_WAVES) k_fft_fwd_stage_q(int m, int s, const uint32_t *__restrict__ A,
-                                                         uint32_t *__restrict__ B, const uint64_t *__restrict__ tw,
-                                                         uint32_t *__restrict__ scratch, int quads) {
-  using F = typename C::Fp;
-  __shared__ uint32_t park_lds[256 * xw<F>()];  // xyzz_add_quad's doubling fallback, per lane
-  uint32_t *park = park_lds + threadIdx.x * xw<F>();
-  const int q = (int)(threadIdx.x & 3);
-  const size_t gq = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-  uint32_t *tab = scratch + gq * 16 * xw<F>();
-  const int half = 1 << (s - 1);
-  const size_t nb = (size_t)1 << (m - 1);
-  for (size_t b = gq; b < nb; b += (size_t)quads) {  // quad-uniform
-    const size_t blk = b >> (s - 1), j = b & (half - 1);
-    const size_t k0 = (blk << s) + j;
-    Xyzz<F> u, v, t;
-    xyzz_load(v, A + (k0 + half) * xw<F>());
-    if (j == 0) t = v;
-    else xyzz_scl_quad(t, v, tw + (j << (m - s)) * 4, tab, park);
-    xyzz_load(u, A + k0 * xw<F>());  // after the multiplication: not live across it
-    Xyzz<F> x = u, nt = t;
-    xyzz_add_quad(x, t, park);
-    fe_neg(nt.Y, t.Y);
-    xyzz_add_quad(u, nt, park);
-    xyzz_store_quad(B + k0 * xw<F>(), x, q);
-    xyzz_store_quad(B + (k0 + half) * xw<F>(), u, q);
-  }
-}
-
-template <class C>
-__global__ void __launch_bounds__(256, ZK_FFT_QUAD_WAVES) k_fft_inv_stage_q(int m, int s, const uint32_t *__restrict__ A,
-                                                         uint32_t *__restrict__ B, const uint64_t *__restrict__ tw,
-                                                         uint32_t *__restrict__ scratch, int quads) {
-  using F = typename C::Fp;
-  __shared__ uint32_t park_lds[256 * xw<F>()];
-  uint32_t *park = park_lds + threadIdx.x * xw<F>();
-  const int q = (int)(threadIdx.x & 3);
-  const size_t gq = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
-  uint32_t *tab = scratch + gq * 16 * xw<F>();
-  const int half = 1 << (s - 1);
-  const size_t no = (size_t)1 << m;
-  for (size_t o = gq; o < no; o += (size_t)quads) {  // quad-uniform
-    const size_t b = o >> 1;
-    const int which = (int)(o & 1);
-    const size_t blk = b >> (s - 1), j = b & (half - 1);
-    const size_t k0 = (blk << s) + j;
-    Xyzz<F> u, v, t;
-    xyzz_load(u, A + k0 * xw<F>());
-    xyzz_load(v, A + (k0 + half) * xw<F>());
-    if (which) fe_neg(v.Y, v.Y);
-    xyzz_add_quad(u, v, park);
-    xyzz_scl_quad(t, u, tw + (which ? (j << (m - s)) : 0) * 4, tab, park);  // tw[0] = 1/2
-    xyzz_store_quad(B + (k0 + (which ? half : 0)) * xw<F>(), t, q);
-  }
-}
-
 // tw[e] = std(scale * base^e) for e < cnt (base, scale: Fr reference Montgomery form)
 template <class Fr>
 __global__ void __launch_bounds__(256) k_fft_tw(int cnt, W6 base, W6 scale, uint64_t *__restrict__ tw) {
@@ -550,18 +409,15 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   ZK_REQUIRE(m >= 0 && m <= 26, "G1 fft: log2 size out of range (0..26)");
   hipStream_t st = dev.stream;
   const size_t N = (size_t)1 << m;
-  // scalar-multiplication lanes are grid-strided so the per-lane table scratch stays bounded;
-  // quad mode: 4 lanes per multiplication, at most 2^16 quads (16 table entries each)
-  static const bool quad_mode = [] {
-    const char *e = getenv("ZK_FFT_QUAD");  // A/B hook: 0 = one lane per multiplication (round 3)
-    return !(e && e[0] == '0');
-  }();
+  // scalar-multiplication lanes are grid-strided so the per-lane table scratch stays bounded.
+  // (Round 4 measured quad-cooperative stages -- 4 lanes per multiplication, signed 5-bit
+  // windows, xyzz_dbl_quad / xyzz_add_quad: BLS12-381 2^16 forward 50 vs 55 ms, inverse 102 vs
+  // 61 ms; at 1-2 waves per SIMD the quads' 4x lanes take extra rounds, profiles/r04g_*.)
   const size_t work = inverse ? N : N / 2;
-  const size_t cap = quad_mode ? (1u << 16) : (1u << 17);
-  size_t lanes = (work < cap ? work : cap) * (quad_mode ? 4 : 1);
+  size_t lanes = work < (1u << 17) ? work : (1u << 17);
   lanes = (lanes + 255) & ~(size_t)255;
   if (lanes == 0) lanes = 256;
-  const size_t tab_per_lane = quad_mode ? 4 : 15;  // table words per lane, in XYZZ units
+  const size_t tab_per_lane = 15;  // table points per lane
   const size_t tw_cnt = N > 1 ? N / 2 : 1;
   dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 2 * N * xw<F>() * 4 + lanes * tab_per_lane * xw<F>() * 4 +
                     tw_cnt * 32 + N * NP * 8 + (1 << 20));
@@ -602,13 +458,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
     uint32_t *in = A, *out = B;
     for (int k = 0; k < m; k++) {
       const int s = inverse ? m - k : k + 1;
-      if (quad_mode && inverse)
-        hipLaunchKernelGGL(k_fft_inv_stage_q<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, tw, scratch,
-                           (int)(lanes / 4));
-      else if (quad_mode)
-        hipLaunchKernelGGL(k_fft_fwd_stage_q<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, tw, scratch,
-                           (int)(lanes / 4));
-      else if (inverse)
+      if (inverse)
         hipLaunchKernelGGL(k_fft_inv_stage<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, tw, scratch, (int)lanes);
       else
         hipLaunchKernelGGL(k_fft_fwd_stage<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, tw, scratch, (int)lanes);

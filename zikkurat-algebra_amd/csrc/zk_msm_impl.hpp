@@ -979,8 +979,11 @@ __global__ void __launch_bounds__(256) k_ysum(const uint32_t *__restrict__ bucke
 //     For G1 the fold's additions are quad-cooperative (xyzz_add_quad, 64 per round).
 //     The next bucket's emptiness test (and, with PF, its data) is loaded one iteration
 //     ahead: at one or two waves per SIMD nothing else hides those latencies.
+#ifndef ZK_YSUM_WAVES
+#define ZK_YSUM_WAVES 1  // waves per SIMD k_ysum2 is compiled for (A/B hook)
+#endif
 template <class C, bool PF>
-__global__ void __launch_bounds__(256) k_ysum2(const uint32_t *__restrict__ buckets,
+__global__ void __launch_bounds__(256, ZK_YSUM_WAVES) k_ysum2(const uint32_t *__restrict__ buckets,
                                                const uint32_t *__restrict__ offsets,
                                                const uint8_t *__restrict__ filled, int W, int c, int l0,
                                                SegRegion r0, SegRegion r1, uint32_t *__restrict__ Y) {

@@ -1,5 +1,5 @@
 // zk_quad.hpp -- quad-cooperative XYZZ point operations for latency-bound phases (the MSM's
-// Y-sum fold and job sums, the group FFT's scalar multiplications): the 4 lanes of an aligned
+// Y-sum fold, the level-0 stitch and the job sums): the 4 lanes of an aligned
 // quad hold the operands REPLICATED and split one point operation's products by dependency
 // level, exchanging results with DPP quad broadcasts, so an operation costs its dependency
 // depth in product latencies instead of its product count.
@@ -113,50 +113,6 @@ __device__ __forceinline__ void xyzz_store_quad(uint32_t *__restrict__ p, const 
   Fe<F> c;
   fe_sel4(c, a.X, a.Y, a.ZZ, a.ZZZ, q);
   fe_store_u(p + q * F::SN, c);
-}
-
-// Quad-cooperative doubling (dbl-2008-s-1, a = 0): 9 products in 3 dependency levels
-//   L1: V = U^2 (U = 2Y), X^2
-//   L2: W = U V, S = X V, M^2 (M = 3 X^2), ZZ3 = V ZZ
-//   L3: M (S - X3), W Y, ZZZ3 = W ZZZ
-// Inputs / outputs replicated over the quad.  Infinity stays infinity (no 2-torsion on the G1
-// curves: their group orders are odd).
-template <class F>
-__device__ __forceinline__ void xyzz_dbl_quad(Xyzz<F> &acc) {
-  if (xyzz_is_inf(acc)) return;
-  const int q = (int)(threadIdx.x & 3);
-  Fe<F> U, x, y, m;
-  fe_add(U, acc.Y, acc.Y);
-  fe_sel4(x, U, acc.X, U, acc.X, q);
-  fe_sqr(m, x);  // q0: V, q1: X^2
-  Fe<F> V, M;
-  fe_bcast<0>(V, m);
-  {
-    Fe<F> x2;
-    fe_bcast<1>(x2, m);
-    fe_mul3(M, x2);
-  }
-  fe_sel4(x, U, acc.X, M, V, q);
-  fe_sel4(y, V, V, M, acc.ZZ, q);
-  fe_mul(m, x, y);  // q0: W, q1: S, q2: M^2, q3: ZZ3
-  Fe<F> W, S, MM, ZZ3, X3, t;
-  fe_bcast<0>(W, m);
-  fe_bcast<1>(S, m);
-  fe_bcast<2>(MM, m);
-  fe_bcast<3>(ZZ3, m);
-  fe_sub(t, MM, S);
-  fe_sub(X3, t, S);  // X3 = M^2 - 2S
-  fe_sub(t, S, X3);
-  fe_sel4(x, M, W, W, M, q);
-  fe_sel4(y, t, acc.Y, acc.ZZZ, t, q);
-  fe_mul(m, x, y);  // q0: M (S - X3), q1: W Y, q2: ZZZ3
-  Fe<F> a0, a1;
-  fe_bcast<0>(a0, m);
-  fe_bcast<1>(a1, m);
-  fe_sub(acc.Y, a0, a1);
-  fe_bcast<2>(acc.ZZZ, m);
-  acc.X = X3;
-  acc.ZZ = ZZ3;
 }
 
 }  // namespace zk

@@ -286,8 +286,10 @@ def main():
                 "random order-r subgroup points P0+i*H in affine Montgomery form)",
         "config": {"workload": workload, "curve": curve, "pairs_total": n_total, "pairs_per_gpu": n_local,
                    "scalars": "Fr Montgomery (Haskell msm path)", "window_c": c,
-                   "parallelism": f"shard{world} (contiguous chunks; partial sums exchanged by the library's "
-                                  f"RCCL all-gather over xGMI)" if dist.comm else "single"},
+                   "parallelism": (f"shard{world} (contiguous chunks; partial sums exchanged by the library's "
+                                   f"RCCL all-gather over xGMI)" if dist.comm else
+                                   f"shard{world} (contiguous chunks; CPU gloo exchange, rehearsal)")
+                   if dist.comm or world > 1 else "single"},
         "parity_vs_reference": parity,
         "parity_key": key if parity is not None else None,
         "input_gen_s": gen_s,
@@ -347,7 +349,7 @@ def bench_config5(zk, args, dist):
            "kernel_ms_max_over_ranks": accum_s * 1e3, "parity_vs_reference": parity,
            "parity_key": "config5_bls12_381_msm_2^26", "input_gen_s": gen_s,
            "exchange": "zkg_g1_msm_device_sharded (ncclAllGather of the partial sums on the library's stream)"
-           if dist.comm else "none (one GPU)"}
+           if dist.comm else ("torch.distributed gloo all-gather on the CPU (rehearsal)" if world > 1 else "none (one GPU)")}
     roof = msm_rooflines(curve, hi - lo, c, accum_s, rocprof=False)
     out["roofline"] = roof["roofline"]
     if "valu_roofline" in roof:

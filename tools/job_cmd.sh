@@ -10,3 +10,5 @@ import sys; sys.argv=['x']; sys.path.insert(0,'tools'); import sweep_window as s
     done
   done
 done
+unset ZK_LIB_PATH
+timeout -k 10 200 python -u tools/fft_time.py 16 2 2>&1 | grep -v amdgpu.ids || exit 1

@@ -20,8 +20,9 @@
 // exact per-level scalars, not only on their product mod r.  This implementation applies
 // the same per-level scalars at the same positions (iterative DIT / DIF over HBM,
 // ping-pong buffers), so its output is bit-identical for every on-curve input.
-// Scalar multiplication: fixed 4-bit windows, MSB first, 15-entry table per lane in
-// global scratch (no lane divergence on the digit: every window does one table add).
+// Scalar multiplication (xyzz_scl): Jacobian accumulator, signed 5-bit windows MSB first, a
+// 16-entry table per lane in global scratch (no lane divergence on the digit: every window does
+// one table add).
 // Outputs are normalised (Z = 1, infinity = (0:1:0)) as the reference does (:719, :785).
 #include "zk_curve.hpp"
 #include "zk_host.hpp"
@@ -214,37 +215,191 @@ __device__ __forceinline__ void xyzz_neg(Xyzz<F> &r, const Xyzz<F> &a) {
   fe_neg(r.Y, a.Y);
 }
 
-// r = k * P, k a 256-bit integer (4 u64), fixed 4-bit windows MSB first; tab = this lane's
-// 15-point scratch table (tab[d-1] = d P)
+// Scalar multiplication r = k P for the group FFT (k a 256-bit integer, 4 u64), computed with
+// the accumulator in JACOBIAN coordinates: the chain is 255 doublings, and a Jacobian doubling
+// (dbl-2009-l, a = 0) is 7 products against XYZZ's 9; additions take the table entry with its
+// Z^2, Z^3 cached (add-1998-cmo-2: 14 products, as XYZZ's).  Digits: signed 5-bit windows
+// (K = k + sum_i 16 * 32^i, digit i = bits [5i, 5i + 5) of K minus 16, in [-16, 15]; K < 2^260
+// as k < 2^256 - 2^255), so at most 52 additions instead of 64 with a 16-point table.
+// 255 x 7 + 52 x 14 + table 241 = ~2750 products per multiplication (was ~3350).
 template <class F>
-__device__ void xyzz_scl(Xyzz<F> &r, const Xyzz<F> &P, const uint64_t *k, uint32_t *__restrict__ tab) {
+struct Jac {
+  Fe<F> X, Y, Z;  // x = X / Z^2, y = Y / Z^3; Z = 0: infinity
+};
+template <class F>
+__device__ __forceinline__ void jac_dbl(Jac<F> &p) {  // in place; infinity stays infinity
+  Fe<F> A, B, C, D, E, t, u;
+  fe_sqr(A, p.X);
+  fe_sqr(B, p.Y);
+  fe_sqr(C, B);
+  fe_add(t, p.X, B);
+  fe_sqr(u, t);
+  fe_sub(u, u, A);
+  fe_sub(u, u, C);
+  fe_add(D, u, u);          // D = 2((X + B)^2 - A - C)
+  fe_mul3(E, A);            // E = 3A
+  fe_sqr(t, E);             // F = E^2
+  fe_sub(t, t, D);
+  Fe<F> X3;
+  fe_sub(X3, t, D);         // X3 = F - 2D
+  fe_mul(u, p.Y, p.Z);
+  fe_add(p.Z, u, u);        // Z3 = 2 Y Z
+  fe_sub(t, D, X3);
+  fe_mul(u, E, t);          // E (D - X3)
+  fe_add(C, C, C);
+  fe_add(C, C, C);
+  fe_add(C, C, C);          // 8C
+  fe_sub(p.Y, u, C);
+  p.X = X3;
+}
+// table entry: the point and its Z^2, Z^3
+template <class F>
+struct JacC {
+  Fe<F> X, Y, Z, ZZ, ZZZ;
+};
+template <class F>
+__device__ __forceinline__ void jac_cache(JacC<F> &c, const Jac<F> &p) {
+  c.X = p.X;
+  c.Y = p.Y;
+  c.Z = p.Z;
+  fe_sqr(c.ZZ, p.Z);
+  fe_mul(c.ZZZ, c.ZZ, p.Z);
+}
+template <class F>
+__device__ __forceinline__ bool jac_is_inf(const Jac<F> &p) { return fe_is_zero(p.Z); }
+// acc += b (b cached, b not infinity); all special cases handled
+template <class F>
+__device__ __forceinline__ void jac_add_cached(Jac<F> &acc, const JacC<F> &b) {
+  if (jac_is_inf(acc)) {
+    acc.X = b.X;
+    acc.Y = b.Y;
+    acc.Z = b.Z;
+    return;
+  }
+  Fe<F> Z1Z1, U1, U2, S1, S2, H, r, t;
+  fe_sqr(Z1Z1, acc.Z);
+  fe_mul(U1, acc.X, b.ZZ);
+  fe_mul(U2, b.X, Z1Z1);
+  fe_mul(S1, acc.Y, b.ZZZ);
+  fe_mul(t, acc.Z, Z1Z1);
+  fe_mul(S2, b.Y, t);
+  fe_sub(H, U2, U1);
+  fe_sub(r, S2, S1);
+  if (fe_is_zero(H)) {
+    if (fe_is_zero(r)) jac_dbl(acc);  // acc == b
+    else fe_zero(acc.Z);              // acc == -b
+    return;
+  }
+  Fe<F> HH, HHH, V, X3;
+  fe_sqr(HH, H);
+  fe_mul(HHH, H, HH);
+  fe_mul(V, U1, HH);
+  fe_sqr(t, r);
+  fe_sub(t, t, HHH);
+  fe_sub(t, t, V);
+  fe_sub(X3, t, V);         // X3 = r^2 - HHH - 2V
+  fe_sub(t, V, X3);
+  fe_mul(V, r, t);          // r (V - X3)
+  fe_mul(t, S1, HHH);
+  fe_sub(acc.Y, V, t);
+  fe_mul(t, acc.Z, b.Z);
+  fe_mul(acc.Z, t, H);      // Z3 = Z1 Z2 H
+  acc.X = X3;
+}
+template <class F>
+__device__ __forceinline__ void jacc_store(uint32_t *p, const JacC<F> &c) {
+  fe_store_u(p + 0 * F::SN, c.X);
+  fe_store_u(p + 1 * F::SN, c.Y);
+  fe_store_u(p + 2 * F::SN, c.Z);
+  fe_store_u(p + 3 * F::SN, c.ZZ);
+  fe_store_u(p + 4 * F::SN, c.ZZZ);
+}
+template <class F>
+__device__ __forceinline__ void jacc_load(JacC<F> &c, const uint32_t *p) {
+  fe_load_u(c.X, p + 0 * F::SN);
+  fe_load_u(c.Y, p + 1 * F::SN);
+  fe_load_u(c.Z, p + 2 * F::SN);
+  fe_load_u(c.ZZ, p + 3 * F::SN);
+  fe_load_u(c.ZZZ, p + 4 * F::SN);
+}
+constexpr int SCL_TAB = 16;                                  // table entries d P, d = 1..16
+template <class F>
+constexpr int scl_tab_words() { return SCL_TAB * 5 * F::SN; }  // u32 words of one lane's table
+// window i (5 bits) of the 261-bit K held in 5 u64 words
+__device__ __forceinline__ uint32_t win5(const uint64_t *K, int i) {
+  const int b = 5 * i, w = b >> 6, o = b & 63;
+  uint64_t v = K[w] >> o;
+  if (o > 59 && w < 4) v |= K[w + 1] << (64 - o);
+  return (uint32_t)v & 31u;
+}
+template <class F>
+__device__ __forceinline__ void xyzz_scl(Xyzz<F> &r, const Xyzz<F> &P, const uint64_t *k, uint32_t *__restrict__ tab) {
+  if (xyzz_is_inf(P)) {
+    r = P;
+    return;
+  }
+  {  // P in Jacobian form: Z' = ZZ ZZZ, X' = X ZZ ZZZ^2, Y' = Y ZZZ^4 (valid XYZZ has ZZ^3 = ZZZ^2)
+    Jac<F> p, acc;
+    Fe<F> z2, z4, t;
+    fe_sqr(z2, P.ZZZ);
+    fe_mul(t, P.X, P.ZZ);
+    fe_mul(p.X, t, z2);
+    fe_sqr(z4, z2);
+    fe_mul(p.Y, P.Y, z4);
+    fe_mul(p.Z, P.ZZ, P.ZZZ);
+    JacC<F> pc, c;
+    jac_cache(pc, p);
+    jacc_store(tab, pc);
+    acc = p;
+    jac_dbl(acc);
+    jac_cache(c, acc);
+    jacc_store(tab + 1 * 5 * F::SN, c);
+    for (int d = 3; d <= SCL_TAB; d++) {
+      jac_add_cached(acc, pc);
+      jac_cache(c, acc);
+      jacc_store(tab + (size_t)(d - 1) * 5 * F::SN, c);
+    }
+  }
+  uint64_t K[5];
   {
-    Xyzz<F> acc = P;
-    xyzz_store(tab, acc);
-    for (int d = 2; d <= 15; d++) {
-      if (d == 2) xyzz_dbl(acc, P);
-      else xyzz_add(acc, P);
-      xyzz_store(tab + (size_t)(d - 1) * xw<F>(), acc);
+    const uint64_t H[5] = {0x0842108421084210ull, 0x1084210842108421ull, 0x2108421084210842ull,
+                           0x4210842108421084ull, 0x8ull};
+    uint64_t cy = 0;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      const uint64_t a = j < 4 ? k[j] : 0, s1 = a + H[j];
+      const uint64_t c1 = s1 < a ? 1 : 0, s2 = s1 + cy;
+      K[j] = s2;
+      cy = c1 | (s2 < s1 ? 1 : 0);
     }
   }
-  Xyzz<F> acc;
-  xyzz_set_inf(acc);
-  for (int w = 63; w >= 0; w--) {
-    if (w != 63) {
-      for (int q = 0; q < 4; q++) {
-        Xyzz<F> t;
-        xyzz_dbl(t, acc);
-        acc = t;
-      }
-    }
-    const uint32_t d = (uint32_t)(k[w >> 4] >> ((w & 15) * 4)) & 15u;
+  Jac<F> acc;
+  fe_one(acc.X);
+  fe_one(acc.Y);
+  fe_zero(acc.Z);
+  for (int i = 51; i >= 0; i--) {
+    if (i != 51)
+      for (int z = 0; z < 5; z++) jac_dbl(acc);
+    const int d = (int)win5(K, i) - 16;
     if (d) {
-      Xyzz<F> e;
-      xyzz_load(e, tab + (size_t)(d - 1) * xw<F>());
-      xyzz_add(acc, e);
+      JacC<F> e;
+      jacc_load(e, tab + (size_t)((d < 0 ? -d : d) - 1) * 5 * F::SN);
+      if (d < 0) {
+        Fe<F> ny;
+        fe_neg(ny, e.Y);
+        e.Y = ny;
+      }
+      jac_add_cached(acc, e);
     }
   }
-  r = acc;
+  if (jac_is_inf(acc)) {
+    xyzz_set_inf(r);
+    return;
+  }
+  r.X = acc.X;
+  r.Y = acc.Y;
+  fe_sqr(r.ZZ, acc.Z);
+  fe_mul(r.ZZZ, r.ZZ, acc.Z);
 }
 
 // forward DIT stage s (block 2^s): lane = butterfly (blk, j); t = w_s^j v (w_s^j = tw[j 2^(m-s)],
@@ -266,7 +421,7 @@ __global__ void __launch_bounds__(256) k_fft_fwd_stage(int m, int s, const uint3
       t = v;
     } else {
       const uint64_t *k = tw + (j << (m - s)) * 4;
-      xyzz_scl(t, v, k, scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 15 * xw<F>());
+      xyzz_scl(t, v, k, scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>());
     }
     Xyzz<F> x = u, nt;
     xyzz_add(x, t);
@@ -302,7 +457,7 @@ __global__ void __launch_bounds__(256) k_fft_inv_stage(int m, int s, const uint3
       xyzz_add(u, nv);
     }
     const uint64_t *k = tw + (which ? (j << (m - s)) : 0) * 4;  // tw[0] = 1/2
-    xyzz_scl(t, u, k, scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 15 * xw<F>());
+    xyzz_scl(t, u, k, scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>());
     xyzz_store(B + (k0 + (which ? half : 0)) * xw<F>(), t);
   }
 }
@@ -417,9 +572,8 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   size_t lanes = work < (1u << 17) ? work : (1u << 17);
   lanes = (lanes + 255) & ~(size_t)255;
   if (lanes == 0) lanes = 256;
-  const size_t tab_per_lane = 15;  // table points per lane
   const size_t tw_cnt = N > 1 ? N / 2 : 1;
-  dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 2 * N * xw<F>() * 4 + lanes * tab_per_lane * xw<F>() * 4 +
+  dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 2 * N * xw<F>() * 4 + lanes * scl_tab_words<F>() * 4 +
                     tw_cnt * 32 + N * NP * 8 + (1 << 20));
   dev.arena.reset();
   const uint64_t *ds = src;
@@ -432,7 +586,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   }
   uint32_t *A = dev.arena.take<uint32_t>(N * xw<F>());
   uint32_t *B = dev.arena.take<uint32_t>(N * xw<F>());
-  uint32_t *scratch = dev.arena.take<uint32_t>(lanes * tab_per_lane * xw<F>());
+  uint32_t *scratch = dev.arena.take<uint32_t>(lanes * scl_tab_words<F>());
   uint64_t *tw = dev.arena.take<uint64_t>(tw_cnt * 4);
   uint64_t *nscratch = dev.arena.take<uint64_t>(N * NP);
 

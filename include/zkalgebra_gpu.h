@@ -12,8 +12,10 @@
  *   projective G1 = X || Y || Z (x = X/Z, y = Y/Z), Jacobian = X || Y || Z (x = X/Z^2).
  * All buffers are caller-owned and are not retained after the call returns.
  * Every call is synchronous and thread-safe.  There are no error codes on the
- * reference ABI: on a device error the library prints a message and aborts (the
+ * reference ABI: by default, on a device error the library prints a message and aborts (the
  * reference asserts, bls12_381_G1_proj.c:518,632) -- it never falls back to a CPU path.
+ * zkg_set_error_mode(1) makes errors recoverable: the failing call prints the message,
+ * returns early (outputs unspecified) and zkg_last_error() reports it to the calling thread.
  *
  * Projective / Jacobian outputs are returned NORMALISED (Z = 1, or the canonical
  * infinity (0:1:0) / Jacobian (1:1:0)); they are equal as points to the reference's
@@ -200,6 +202,11 @@ ZKG_API uint8_t bls12_381_poly_mont_quot_by_vanishing( int n1, const uint64_t *s
 #define ZKG_BLS12_381 1
 
 ZKG_API const char *zkg_version(void);
+/* error channel: mode 0 = print and abort on a device error (default, reference-like),
+ * 1 = print, return from the failing call (outputs unspecified) and record the message;
+ * zkg_last_error returns 1 and copies the calling thread's last message (cleared), else 0 */
+ZKG_API void zkg_set_error_mode(int mode);
+ZKG_API int zkg_last_error(char *msg, size_t cap);
 ZKG_API int zkg_device_count(void);
 ZKG_API void zkg_set_device(int device);           /* binds the calling thread */
 ZKG_API void *zkg_device_malloc(size_t bytes);

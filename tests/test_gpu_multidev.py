@@ -33,6 +33,30 @@ def test_device_set_api(gpu):
     assert gpu.get_devices() == []
 
 
+@pytest.mark.parametrize("curve", CURVES)
+def test_one_entry_device_set(gpu, oracle, curve):
+    """a one-entry set pins the host-buffer MSM and NTT to that device: get_devices
+    reports it and the results are unchanged (on the one-GPU box the entry is device 0, so this
+    runs the pinned path -- hipSetDevice to the listed device around the call)"""
+    n = 5000
+    sc = gpu.gen_fr(curve, 81, n)
+    pts = gpu.gen_points(curve, 82, n)
+    m = 16
+    sg = gpu.get_fft_subgroup(curve, m)
+    x = gpu.gen_fr(curve, 83, 1 << m)
+    want_msm = gpu.msm_affine(curve, sc, pts)
+    want_ntt = gpu.forward_ntt(sg, x)
+    gpu.set_devices([0])
+    try:
+        assert gpu.get_devices() == [0]
+        assert np.array_equal(gpu.msm_affine(curve, sc, pts), want_msm)
+        assert np.array_equal(gpu.forward_ntt(sg, x), want_ntt)
+        assert np.array_equal(gpu.inverse_ntt(sg, want_ntt), x)
+    finally:
+        gpu.set_devices([])
+    assert np.array_equal(want_msm, oracle.msm(curve, sc, pts, mont=True))
+
+
 @pytest.mark.parametrize("shards", [2, 8], indirect=True)
 @pytest.mark.parametrize("curve", CURVES)
 def test_sharded_golden(gpu, curve, shards):

@@ -1,14 +1,10 @@
-# scratch commands of the current GPU experiment (run by tools/gpu_job.sh step "cmd")
-# r04h: Y sums at 2 waves per SIMD (131072 lanes, 8 buckets each; quad fold) vs the default
+# r04k: window sweep for 2^17..2^19 (the Y sums cost the same 0.32 ms at c = 16 from 2^18 to 2^20)
 cd "$GRAFT_REPO_ROOT"
-for rep in 1 2 3; do
-  for v in new ysA ysB; do
-    if [ $v = new ]; then unset ZK_LIB_PATH; else export ZK_LIB_PATH=$PWD/variants/$v/libzkalgebra_gpu.so; fi
-    for lg in 20 16; do
-      timeout -k 10 120 python -u -c "
-import sys; sys.argv=['x']; sys.path.insert(0,'tools'); import sweep_window as s; s.run('bls12_381', $lg, [0], reps=3, profile=True)" 2>&1 | grep -v amdgpu.ids | sed "s/^/[$v] /" | tail -2 || exit 1
-    done
+for rep in 1 2; do
+  for lg in 17 18 19 20; do
+    timeout -k 10 200 python -u tools/sweep_window.py bls12_381 $lg 13 14 15 16 2>&1 | grep -v amdgpu.ids || exit 1
+  done
+  for lg in 17 18 19 20; do
+    timeout -k 10 200 python -u tools/sweep_window.py bn128 $lg 13 14 15 16 2>&1 | grep -v amdgpu.ids || exit 1
   done
 done
-unset ZK_LIB_PATH
-timeout -k 10 200 python -u tools/fft_time.py 16 2 2>&1 | grep -v amdgpu.ids || exit 1

@@ -27,7 +27,12 @@ void msm_entry(int npoints, const uint64_t *expos, const uint64_t *grps, uint64_
   using HF = typename HostOf<C>::Fp;
   constexpr int NP = C::NP64;
   uint64_t proj[3 * NP];
-  msm_g1<C>(npoints, expos, nl, grps, /*host_inputs=*/true, mont, window, proj);
+  bool ok = false;
+  guard([&] {
+    msm_g1<C>(npoints, expos, nl, grps, /*host_inputs=*/true, mont, window, proj);
+    ok = true;
+  });
+  if (!ok) return;  // recoverable error mode: the message is in zkg_last_error
   zkh::Proj<HF> p;
   memcpy(p.X.v, proj, NP * 8);
   memcpy(p.Y.v, proj + NP, NP * 8);
@@ -119,16 +124,16 @@ ZKG_G2_MSM_ENTRIES(bn128, BN254_G2)
 ZKG_G2_MSM_ENTRIES(bls12_381, BLS381_G2)
 
 ZKG_API void bn128_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
-  zk::ntt(ZKG_BN128, m, gen, src, tgt, true, false);
+  guard([&] { zk::ntt(ZKG_BN128, m, gen, src, tgt, true, false); });
 }
 ZKG_API void bn128_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
-  zk::ntt(ZKG_BN128, m, gen, src, tgt, true, true);
+  guard([&] { zk::ntt(ZKG_BN128, m, gen, src, tgt, true, true); });
 }
 ZKG_API void bls12_381_poly_mont_ntt_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
-  zk::ntt(ZKG_BLS12_381, m, gen, src, tgt, true, false);
+  guard([&] { zk::ntt(ZKG_BLS12_381, m, gen, src, tgt, true, false); });
 }
 ZKG_API void bls12_381_poly_mont_ntt_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {
-  zk::ntt(ZKG_BLS12_381, m, gen, src, tgt, true, true);
+  guard([&] { zk::ntt(ZKG_BLS12_381, m, gen, src, tgt, true, true); });
 }
 
 // ---------------------------------------------------------------------------- Part 2
@@ -140,25 +145,37 @@ ZKG_API int zkg_device_count(void) {
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
 }
-ZKG_API void zkg_set_device(int device) { ZK_CHECK(hipSetDevice(device)); }
+ZKG_API void zkg_set_error_mode(int mode) { zk::set_error_mode(mode); }
+ZKG_API int zkg_last_error(char *msg, size_t cap) { return zk::take_last_error(msg, cap); }
+
+ZKG_API void zkg_set_device(int device) {
+  guard([&] { ZK_CHECK(hipSetDevice(device)); });
+}
 ZKG_API void *zkg_device_malloc(size_t bytes) {
-  void *p = nullptr;
-  ZK_CHECK(hipMalloc(&p, bytes ? bytes : 1));
-  return p;
+  return guard_ret<void *>(nullptr, [&] {
+    void *p = nullptr;
+    ZK_CHECK(hipMalloc(&p, bytes ? bytes : 1));
+    return p;
+  });
 }
 ZKG_API void zkg_device_free(void *ptr) {
-  if (ptr) ZK_CHECK(hipFree(ptr));
+  guard([&] {
+    if (ptr) ZK_CHECK(hipFree(ptr));
+  });
 }
 ZKG_API void zkg_memcpy_htod(void *dst, const void *src, size_t bytes) {
-  ZK_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  guard([&] { ZK_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)); });
 }
 ZKG_API void zkg_memcpy_dtoh(void *dst, const void *src, size_t bytes) {
-  ZK_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  guard([&] { ZK_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost)); });
 }
-ZKG_API void zkg_device_synchronize(void) { ZK_CHECK(hipDeviceSynchronize()); }
+ZKG_API void zkg_device_synchronize(void) {
+  guard([&] { ZK_CHECK(hipDeviceSynchronize()); });
+}
 
 ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,
                                const uint64_t *d_grps, uint64_t *tgt_proj, int window_size) {
+  guard([&] {
   int c = window_size <= 0 ? 0 : (window_size < 4 ? 4 : (window_size > 24 ? 24 : window_size));
   if (curve == ZKG_BN128) {
     uint64_t p[12];
@@ -169,10 +186,12 @@ ZKG_API void zkg_g1_msm_device(int curve, int npoints, const uint64_t *d_expos, 
     msm_g1<BLS381>(npoints, d_expos, expo_nlimbs, d_grps, false, expos_mont != 0, c, p);
     zkg_g1_proj_normalize(curve, p, tgt_proj);
   }
+  });
 }
 
 ZKG_API void zkg_g2_msm_device(int curve, int npoints, const uint64_t *d_expos, int expo_nlimbs, int expos_mont,
                                const uint64_t *d_grps, uint64_t *tgt_proj, int window_size) {
+  guard([&] {
   int c = window_size <= 0 ? 0 : (window_size < 4 ? 4 : (window_size > 24 ? 24 : window_size));
   if (curve == ZKG_BN128) {
     uint64_t p[24];
@@ -189,11 +208,12 @@ ZKG_API void zkg_g2_msm_device(int curve, int npoints, const uint64_t *d_expos, 
     zkh::proj_normalize(r, q);
     memcpy(tgt_proj, &r, sizeof r);
   }
+  });
 }
 
 ZKG_API void zkg_ntt_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src,
                             uint64_t *d_tgt) {
-  zk::ntt(curve, m, gen, d_src, d_tgt, false, inverse != 0);
+  guard([&] { zk::ntt(curve, m, gen, d_src, d_tgt, false, inverse != 0); });
 }
 
 }  // extern "C"
@@ -281,9 +301,13 @@ ZKG_API void zkg_arena_set_limit(size_t bytes) { zk::arena_set_limit(bytes); }
 ZKG_API int zkg_msm_last_groups(void) { return zk::msm_last_groups_read(); }
 ZKG_API size_t zkg_msm_workspace_bytes(int curve, int npoints, int expo_nlimbs, int expos_mont, int host_inputs,
                                        int window_size, int groups) {
-  if (curve == ZKG_BN128)
-    return zk::msm_workspace_bytes<BN254>(npoints, expo_nlimbs, expos_mont != 0, host_inputs != 0, window_size, groups);
-  return zk::msm_workspace_bytes<BLS381>(npoints, expo_nlimbs, expos_mont != 0, host_inputs != 0, window_size, groups);
+  return guard_ret<size_t>(0, [&] {
+    if (curve == ZKG_BN128)
+      return zk::msm_workspace_bytes<BN254>(npoints, expo_nlimbs, expos_mont != 0, host_inputs != 0, window_size,
+                                            groups);
+    return zk::msm_workspace_bytes<BLS381>(npoints, expo_nlimbs, expos_mont != 0, host_inputs != 0, window_size,
+                                           groups);
+  });
 }
 
 ZKG_API int zkg_set_devices(const int *ids, int n) { return zk::set_device_set(ids, n); }
@@ -294,6 +318,7 @@ ZKG_API int zkg_get_devices(int *ids, int cap) {
 }
 
 ZKG_API void zkg_release(void) {
+  guard([&] {
   int prev = 0;
   ZK_CHECK(hipGetDevice(&prev));
   for (Device *d : all_devices()) {
@@ -304,6 +329,7 @@ ZKG_API void zkg_release(void) {
     d->release_memory();
   }
   ZK_CHECK(hipSetDevice(prev));
+  });
 }
 
 ZKG_API void zkg_timer_enable(int on) { timer_set_enabled(on != 0); }

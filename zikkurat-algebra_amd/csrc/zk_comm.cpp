@@ -153,14 +153,17 @@ int sharded_msm(int n, const uint64_t *d_expos, int nl, bool mont, const uint64_
 extern "C" {
 
 ZKG_API int zkg_comm_unique_id(void *out) {
+  return guard_ret(-3, [&]() -> int {
   ncclUniqueId id;
   StdoutToStderr quiet;
   ZK_NCCL("ncclGetUniqueId", ncclGetUniqueId(&id));
   memcpy(out, &id, sizeof id);
   return 0;
+  });
 }
 
 ZKG_API int zkg_comm_init(int rank, int world, const void *unique_id) {
+  return guard_ret(-3, [&]() -> int {
   std::lock_guard<std::mutex> lock(g_comm.mu);
   if (g_comm.comm) {
     fprintf(stderr, "[zkalgebra_gpu] zkg_comm_init: a communicator already exists (zkg_comm_destroy first)\n");
@@ -194,9 +197,11 @@ ZKG_API int zkg_comm_init(int rank, int world, const void *unique_id) {
       return -2;
     }
   return 0;
+  });
 }
 
 ZKG_API int zkg_comm_destroy(void) {
+  return guard_ret(-3, [&]() -> int {
   std::lock_guard<std::mutex> lock(g_comm.mu);
   if (!g_comm.comm) return 0;
   OnCommDevice on(g_comm.device);
@@ -215,6 +220,7 @@ ZKG_API int zkg_comm_destroy(void) {
   g_comm.device = -1;
   if (r != ncclSuccess) return report("ncclCommDestroy", r);
   return 0;
+  });
 }
 
 ZKG_API int zkg_comm_rank(void) {
@@ -228,20 +234,25 @@ ZKG_API int zkg_comm_world(void) {
 }
 
 ZKG_API int zkg_comm_allgather(const void *send, void *recv, size_t bytes) {
+  return guard_ret(-3, [&]() -> int {
   std::lock_guard<std::mutex> lock(g_comm.mu);
   if (!g_comm.comm) return -1;
   return allgather_host(send, recv, bytes);
+  });
 }
 
 ZKG_API int zkg_comm_barrier(void) {
+  return guard_ret(-3, [&]() -> int {
   std::lock_guard<std::mutex> lock(g_comm.mu);
   if (!g_comm.comm) return -1;
   std::vector<uint8_t> all((size_t)g_comm.world);
   uint8_t one = 1;
   return allgather_host(&one, all.data(), 1);
+  });
 }
 
 ZKG_API int zkg_comm_max_f64(double *x) {
+  return guard_ret(-3, [&]() -> int {
   std::lock_guard<std::mutex> lock(g_comm.mu);
   if (!g_comm.comm) return -1;
   std::vector<double> all((size_t)g_comm.world);
@@ -249,9 +260,11 @@ ZKG_API int zkg_comm_max_f64(double *x) {
   for (double v : all)
     if (v > *x) *x = v;
   return 0;
+  });
 }
 
 ZKG_API int zkg_g1_comm_sum_partials(int curve, const uint64_t *partials, int count, uint64_t *tgt_proj) {
+  return guard_ret(-3, [&]() -> int {
   std::lock_guard<std::mutex> lock(g_comm.mu);
   if (!g_comm.comm || count < 1) return -1;
   const int NP = curve == ZKG_BN128 ? BN254::NP64 : BLS381::NP64;
@@ -261,17 +274,20 @@ ZKG_API int zkg_g1_comm_sum_partials(int curve, const uint64_t *partials, int co
   if (curve == ZKG_BN128) sum_partials<BN254>(all.data(), count * g_comm.world, tgt_proj);
   else sum_partials<BLS381>(all.data(), count * g_comm.world, tgt_proj);
   return 0;
+  });
 }
 
 ZKG_API int zkg_g1_msm_device_sharded(int curve, int npoints_local, const uint64_t *d_expos, int expo_nlimbs,
                                       int expos_mont, const uint64_t *d_grps, int window_size, int local_shards,
                                       uint64_t *tgt_proj) {
+  return guard_ret(-3, [&]() -> int {
   std::lock_guard<std::mutex> lock(g_comm.mu);
   if (!g_comm.comm || local_shards < 1 || npoints_local < 0 || expo_nlimbs < 1) return -1;
   const int c = window_size <= 0 ? 0 : (window_size < 4 ? 4 : (window_size > 24 ? 24 : window_size));
   if (curve == ZKG_BN128)
     return sharded_msm<BN254>(npoints_local, d_expos, expo_nlimbs, expos_mont != 0, d_grps, c, local_shards, tgt_proj);
   return sharded_msm<BLS381>(npoints_local, d_expos, expo_nlimbs, expos_mont != 0, d_grps, c, local_shards, tgt_proj);
+  });
 }
 
 }  // extern "C"

@@ -164,7 +164,10 @@ __global__ void __launch_bounds__(256) k_digits(const uint64_t *__restrict__ sca
 }
 
 constexpr int MSM_COARSE_BINS = 256;  // coarse bins per window (fewer when B is smaller)
-constexpr int SORT_CHUNK = 4096;      // level-1 entries staged in LDS at a time (16 per thread)
+#ifndef ZK_SORT_CHUNK
+#define ZK_SORT_CHUNK 4096
+#endif
+constexpr int SORT_CHUNK = ZK_SORT_CHUNK;  // level-1 entries staged in LDS at a time (16 per thread)
 constexpr int FINE_LDS_MAX = 8192;    // level-2 bins up to this size are placed in LDS
 constexpr int FINE_LDS_BYTES = 150 * 1024;  // dynamic LDS of k_fine: 2^s counters + staging
 static int fine_stage_cap(int s) {
@@ -1118,7 +1121,11 @@ __global__ void __launch_bounds__(256) k_jobsum_blk(const uint32_t *__restrict__
     xyzz_load(p, Yd + (size_t)v * XW);
     xyzz_add_quad(acc, p, park);
   }
-  for (int h = 32; h >= 1; h >>= 1) {
+  // fold only over the quads that hold items (min(n, 64)): small windows have 8-32 items per job
+  const int act = n < 64 ? n : 64;
+  int h0 = 1;
+  while (2 * h0 < act) h0 <<= 1;
+  for (int h = act > 1 ? h0 : 0; h >= 1; h >>= 1) {
     if (t >= h && t < 2 * h && (threadIdx.x & 3) == 0) xyzz_store(fold + (size_t)(t - h) * XW, acc);
     __syncthreads();
     if (t < h) {
@@ -1763,8 +1770,11 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   uint32_t *pts_int = nullptr;
   PhaseProf prof(st);
   bool inputs_on_aux = false;
-  std::thread copier;
   std::atomic<int> ready_sc[ZK_MSM_SPLITS_MAX], ready_pt[ZK_MSM_SPLITS_MAX];
+  std::string copy_err;  // an Error of the copy thread (recoverable error mode), rethrown after join
+  std::mutex copy_mu;
+  std::vector<std::thread> copier_v;  // the copy thread, joined on every exit (JoinAll)
+  JoinAll join_copier{copier_v};
   uint64_t *pts_ref = nullptr;  // host inputs: the device copy of the caller's (reference-form) points
   if (host_inputs) {
     uint64_t *a = dev.arena.take<uint64_t>((size_t)n * sc_in.stride);
@@ -1791,7 +1801,9 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
     const int stride = sc_in.stride;
     const uint64_t *sc_host = sc_in.data;
     const MsmShape shp = s;
-    copier = std::thread([&dev, st2, NS, shp, a, b, stride, sc_host, points, &ready_sc, &ready_pt] {
+    copier_v.emplace_back([&dev, st2, NS, shp, a, b, stride, sc_host, points, &ready_sc, &ready_pt, &copy_err,
+                           &copy_mu] {
+      catch_into(&copy_err, &copy_mu, [&] {
       ZK_CHECK(hipSetDevice(dev.id));
       for (int h = 0; h < NS; h++) {
         const int lo = shp.split_lo(h), hi = shp.split_lo(h + 1);
@@ -1802,6 +1814,11 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
         const size_t off = (size_t)lo * 2 * C::NP64;
         ZK_CHECK(hipMemcpyAsync(b + off, points + off, (size_t)(hi - lo) * 2 * C::NP64 * 8, hipMemcpyHostToDevice, st2));
         ZK_CHECK(hipEventRecord(dev.split_event(3 * h + 1), st2));
+        ready_pt[h].store(1, std::memory_order_release);
+      }
+      });
+      for (int h = 0; h < NS; h++) {  // after an error too: the waiting pipeline must not spin forever
+        ready_sc[h].store(1, std::memory_order_release);
         ready_pt[h].store(1, std::memory_order_release);
       }
     });
@@ -1838,10 +1855,11 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
     }
     inputs_on_aux = false;
     pass.launch();
-    if (copier.joinable()) copier.join();  // every copy is issued (the stream order does the rest)
+    for (auto &t : copier_v)
+      if (t.joinable()) t.join();  // every copy is issued (the stream order does the rest)
     pass.finish();
+    rethrow_first(copy_err);
   }
-  if (copier.joinable()) copier.join();
   timer_collect(dev);
   const auto t0 = std::chrono::steady_clock::now();
   finish_host<C>(c, W, h, out);
@@ -1912,6 +1930,10 @@ void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool
     // group sum), and the reference's own call is a single chunk (G1_proj.c:630-644).
     std::vector<zkh::Xyzz<HF>> part(G);
     std::vector<std::thread> th;
+    std::string err;
+    std::mutex emu;
+    {
+    JoinAll join_all{th};
     for (int k = 0; k < G; k++) {
       const size_t lo = (size_t)n * k / G, hi = (size_t)n * (k + 1) / G;
       int slot = 0;
@@ -1919,13 +1941,17 @@ void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool
       zkh::xyzz_set_inf(part[k]);
       if (hi == lo) continue;
       th.emplace_back([&, k, lo, hi, slot] {
-        ZK_CHECK(hipSetDevice(set[k]));
-        Device &d = device_context(set[k], slot);
-        std::lock_guard<std::mutex> lock(d.mu);
-        msm_xyzz<C>(d, (int)(hi - lo), scalars + lo * nl, nl, points + lo * 2 * C::NP64, true, mont, window, part[k]);
+        catch_into(&err, &emu, [&] {
+          ZK_CHECK(hipSetDevice(set[k]));
+          Device &d = device_context(set[k], slot);
+          std::lock_guard<std::mutex> lock(d.mu);
+          msm_xyzz<C>(d, (int)(hi - lo), scalars + lo * nl, nl, points + lo * 2 * C::NP64, true, mont, window,
+                      part[k]);
+        });
       });
     }
-    for (auto &t : th) t.join();
+    }  // joined
+    rethrow_first(err);
     zkh::xyzz_set_inf(acc);
     for (int k = 0; k < G; k++) zkh::xyzz_add(acc, acc, part[k]);
   } else if (G == 1) {  // a one-entry set pins the host-buffer MSM to that device

@@ -638,8 +638,12 @@ static void spread_chunk(size_t n, int G, int k, size_t &off, size_t &len) {
 // host -> device-0 buffer `d` (bytes), chunk 0 by dev0's own stream (caller's thread)
 static void spread_in(Device &dev0, const Spread &sp, uint64_t *d, const uint64_t *h, size_t bytes) {
   std::vector<std::thread> th;
+  std::string err;
+  std::mutex emu;
+  {
+  JoinAll join_all{th};
   for (int k = 1; k < sp.G; k++) {
-    th.emplace_back([&, k] {
+    th.emplace_back([&, k] { catch_into(&err, &emu, [&] {
       Device &hk = *sp.helpers[k - 1];
       size_t off, len;
       spread_chunk(bytes, sp.G, k, off, len);
@@ -650,20 +654,25 @@ static void spread_in(Device &dev0, const Spread &sp, uint64_t *d, const uint64_
       if (hk.id == dev0.id) ZK_CHECK(hipMemcpyAsync((char *)d + off, buf, len, hipMemcpyDeviceToDevice, hk.stream));
       else ZK_CHECK(hipMemcpyPeerAsync((char *)d + off, dev0.id, buf, hk.id, len, hk.stream));
       ZK_CHECK(hipStreamSynchronize(hk.stream));
-    });
+    }); });
   }
   size_t off, len;
   spread_chunk(bytes, sp.G, 0, off, len);
   ZK_CHECK(hipMemcpyAsync((char *)d + off, (const char *)h + off, len, hipMemcpyHostToDevice, dev0.stream));
-  for (auto &t : th) t.join();
+  }  // joined
+  rethrow_first(err);
   ZK_CHECK(hipSetDevice(dev0.id));
 }
 
 // device-0 buffer `d` -> host (dev0's stream is idle: the passes have completed)
 static void spread_out(Device &dev0, const Spread &sp, uint64_t *h, const uint64_t *d, size_t bytes) {
   std::vector<std::thread> th;
+  std::string err;
+  std::mutex emu;
+  {
+  JoinAll join_all{th};
   for (int k = 1; k < sp.G; k++) {
-    th.emplace_back([&, k] {
+    th.emplace_back([&, k] { catch_into(&err, &emu, [&] {
       Device &hk = *sp.helpers[k - 1];
       size_t off, len;
       spread_chunk(bytes, sp.G, k, off, len);
@@ -675,12 +684,13 @@ static void spread_out(Device &dev0, const Spread &sp, uint64_t *h, const uint64
       else ZK_CHECK(hipMemcpyPeerAsync(buf, hk.id, (const char *)d + off, dev0.id, len, hk.stream));
       ZK_CHECK(hipMemcpyAsync((char *)h + off, buf, len, hipMemcpyDeviceToHost, hk.stream));
       ZK_CHECK(hipStreamSynchronize(hk.stream));
-    });
+    }); });
   }
   size_t off, len;
   spread_chunk(bytes, sp.G, 0, off, len);
   ZK_CHECK(hipMemcpyAsync((char *)h + off, (const char *)d + off, len, hipMemcpyDeviceToHost, dev0.stream));
-  for (auto &t : th) t.join();
+  }  // joined
+  rethrow_first(err);
   ZK_CHECK(hipSetDevice(dev0.id));
 }
 

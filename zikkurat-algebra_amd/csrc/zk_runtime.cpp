@@ -9,10 +9,28 @@
 
 namespace zk {
 
+static std::atomic<int> g_error_mode{0};
+void set_error_mode(int mode) { g_error_mode.store(mode == 1 ? 1 : 0); }
+
 [[noreturn]] void fatal(const char *what, const char *file, int line) {
-  fprintf(stderr, "[zkalgebra_gpu] fatal: %s (%s:%d)\n", what, file, line);
+  char msg[512];
+  snprintf(msg, sizeof msg, "%s (%s:%d)", what, file, line);
+  fprintf(stderr, "[zkalgebra_gpu] %s: %s\n", g_error_mode.load() ? "error" : "fatal", msg);
   fflush(stderr);
+  if (g_error_mode.load()) throw Error(msg);
   abort();
+}
+
+static thread_local std::string t_last_error;
+void record_error(const char *msg) { t_last_error = msg; }
+int take_last_error(char *msg, size_t cap) {
+  if (t_last_error.empty()) return 0;
+  if (msg && cap) {
+    strncpy(msg, t_last_error.c_str(), cap - 1);
+    msg[cap - 1] = 0;
+  }
+  t_last_error.clear();
+  return 1;
 }
 
 static std::atomic<size_t> g_arena_limit{0};

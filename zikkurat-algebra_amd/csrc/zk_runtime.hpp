@@ -12,19 +12,72 @@
 #include <stdlib.h>
 #include <functional>
 #include <mutex>
+#include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 #include "zk_hostpool.hpp"
 
 namespace zk {
 
-// error handling: no error codes cross the reference ABI (void functions), so a
-// failure on the device path is fatal and loud -- never a silent CPU fallback.
+// error handling: no error codes cross the reference ABI (void functions), so by default a
+// failure on the device path is fatal and loud (the reference asserts) -- never a silent CPU
+// fallback.  zkg_set_error_mode(1) makes it recoverable instead: fatal() throws zk::Error, every
+// C-ABI entry point catches it (guard / guard_ret below), records the message for the calling
+// thread (zkg_last_error) and returns with its outputs unspecified.
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 [[noreturn]] void fatal(const char *what, const char *file, int line);
+void set_error_mode(int mode);  // 0: print and abort (default), 1: throw zk::Error
+void record_error(const char *msg);
+int take_last_error(char *msg, size_t cap);  // 1 and the message if the thread has one (cleared)
+template <class Fn>
+inline void guard(Fn &&fn) {
+  try {
+    fn();
+  } catch (const Error &e) {
+    record_error(e.what());
+  }
+}
+template <class R, class Fn>
+inline R guard_ret(R on_error, Fn &&fn) {
+  try {
+    return fn();
+  } catch (const Error &e) {
+    record_error(e.what());
+    return on_error;
+  }
+}
+// runs fn on a worker thread's behalf: an Error is kept in *err (first one wins, under *mu)
+// instead of escaping the thread; the spawning thread rethrows it after join (rethrow_first)
+template <class Fn>
+inline void catch_into(std::string *err, std::mutex *mu, Fn &&fn) {
+  try {
+    fn();
+  } catch (const Error &e) {
+    std::lock_guard<std::mutex> lock(*mu);
+    if (err->empty()) *err = e.what();
+  }
+}
+inline void rethrow_first(const std::string &err) {
+  if (!err.empty()) throw Error(err);
+}
+// joins every thread of `th` when the scope ends (also while an Error unwinds it)
+struct JoinAll {
+  std::vector<std::thread> &th;
+  ~JoinAll() {
+    for (auto &t : th)
+      if (t.joinable()) t.join();
+  }
+};
 #define ZK_CHECK(x)                                                       \
   do {                                                                    \
     hipError_t e__ = (x);                                                 \
-    if (e__ != hipSuccess) ::zk::fatal(hipGetErrorString(e__), __FILE__, __LINE__); \
+    if (e__ != hipSuccess) {                                              \
+      (void)hipGetLastError(); /* not sticky: later hipGetLastError checks stay clean */ \
+      ::zk::fatal(hipGetErrorString(e__), __FILE__, __LINE__);            \
+    }                                                                     \
   } while (0)
 #define ZK_REQUIRE(cond, msg)                                             \
   do {                                                                    \

@@ -63,7 +63,7 @@ EXTENSION_SYMBOLS = [
     "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
     "zkg_release", "zkg_comm_unique_id", "zkg_comm_init", "zkg_comm_destroy", "zkg_comm_rank", "zkg_comm_world",
     "zkg_comm_allgather", "zkg_comm_barrier", "zkg_comm_max_f64", "zkg_g1_comm_sum_partials",
-    "zkg_g1_msm_device_sharded",
+    "zkg_g1_msm_device_sharded", "zkg_set_error_mode", "zkg_last_error",
 ]
 
 _lib = None
@@ -104,6 +104,7 @@ def load():
                                           ctypes.c_void_p, U64P, U64P, ctypes.c_void_p]
         lib.zkg_arr_dot_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, U64P]
         lib.zkg_arr_powers_device.argtypes = [ctypes.c_int, ctypes.c_int, U64P, U64P, ctypes.c_void_p]
+        lib.zkg_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         lib.zkg_comm_unique_id.argtypes = [ctypes.c_void_p]
         lib.zkg_comm_init.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         lib.zkg_comm_allgather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
@@ -603,6 +604,18 @@ def get_devices():
     arr = (ctypes.c_int * 64)()
     n = load().zkg_get_devices(arr, 64)
     return list(arr[:min(n, 64)])
+
+
+def set_error_mode(recoverable):
+    """zkg_set_error_mode: False = abort on a device error (default), True = the failing call
+    returns and last_error() reports it"""
+    load().zkg_set_error_mode(1 if recoverable else 0)
+
+
+def last_error():
+    """the calling thread's last recorded library error (cleared), or None"""
+    buf = ctypes.create_string_buffer(512)
+    return buf.value.decode() if load().zkg_last_error(buf, 512) else None
 
 
 def release():

@@ -321,6 +321,9 @@ ZKG_API void zkg_ntt_set_table_max(size_t entries);
 ZKG_API void zkg_arena_set_limit(size_t bytes);
 /* window groups (pipeline passes) of the most recent single-device MSM pass */
 ZKG_API int zkg_msm_last_groups(void);
+/* 1 when the most recent group FFT (G1 fft / ifft) ran the GLV stages (every input point in the
+ * order-r subgroup), 0 when it ran the integer-scalar stages */
+ZKG_API int zkg_g1_fft_last_glv(void);
 /* device bytes of one G1 MSM's working set (the arena it reserves) with its windows split into
  * `groups` passes; window_size <= 0: the default window */
 ZKG_API size_t zkg_msm_workspace_bytes(int curve, int npoints, int expo_nlimbs, int expos_mont, int host_inputs,

@@ -87,8 +87,11 @@ def test_batch_to_affine(gpu, oracle, reference, curve, n):
 
 
 @pytest.mark.parametrize("curve", CURVES)
-@pytest.mark.parametrize("m", [0, 1, 2, 3, 5, 8])
+@pytest.mark.parametrize("m", [0, 1, 2, 3, 5, 8, 10])
 def test_fft_vs_reference(gpu, oracle, reference, curve, m):
+    """subgroup points (with infinities): the GLV stages run (pair-split multiplications,
+    decomposed twiddles, the inverse's 1/2 per level deferred to one N^-1) and the normalised
+    output equals the reference's bit for bit"""
     n = 1 << m
     pts = projective(gpu, oracle, curve, n, 200 + m, n_inf=min(2, n))
     sg = gpu.get_fft_subgroup(curve, m)
@@ -96,6 +99,22 @@ def test_fft_vs_reference(gpu, oracle, reference, curve, m):
         want = np.zeros_like(pts)
         ref_call(reference, curve, name, m, sg.gen_array(), pts, want)
         assert np.array_equal(f(sg, pts), want), (name, m)
+        assert gpu.g1_fft_last_glv() == (1 if m > 0 else 0), (name, m)
+
+
+def test_fft_one_nonsubgroup_point_falls_back(gpu, oracle, reference):
+    """BLS12-381: one input outside the r-subgroup among subgroup points -> the membership check
+    fails and the integer-scalar stages run (the reference's exact schedule)"""
+    curve, m = "bls12_381", 6
+    n = 1 << m
+    pts = projective(gpu, oracle, curve, n, 250, n_inf=1)
+    pts[5] = gpu.batch_from_affine(curve, bls_nonsubgroup_points(1, 251))[0]
+    sg = gpu.get_fft_subgroup(curve, m)
+    for name, f in (("G1_proj_fft_forward", gpu.forward_fft), ("G1_proj_fft_inverse", gpu.inverse_fft)):
+        want = np.zeros_like(pts)
+        ref_call(reference, curve, name, m, sg.gen_array(), pts, want)
+        assert np.array_equal(f(sg, pts), want), name
+        assert gpu.g1_fft_last_glv() == 0, name
 
 
 @pytest.mark.parametrize("m", [1, 3, 6])
@@ -109,6 +128,7 @@ def test_fft_nonsubgroup_points_bls(gpu, reference, m):
         want = np.zeros_like(proj)
         ref_call(reference, curve, name, m, sg.gen_array(), proj, want)
         assert np.array_equal(f(sg, proj), want), (name, m)
+        assert gpu.g1_fft_last_glv() == 0, (name, m)
 
 
 @pytest.mark.parametrize("curve", CURVES)

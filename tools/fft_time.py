@@ -29,6 +29,12 @@ for curve in ("bls12_381", "bn128"):
             lib.zkg_g1_fft_device(zk.CURVE_ID[curve], inv, m, zk._p(g), d_in.ptr, d_out.ptr)
         lib.zkg_device_synchronize()
         out[name] = (time.perf_counter() - t) / reps * 1e3
+    glv = zk.g1_fft_last_glv() if hasattr(zk, "g1_fft_last_glv") else "?"
     d_in.free()
     d_out.free()
-    print(f"{curve} 2^{m} group FFT: forward {out['forward']:.2f} ms, inverse {out['inverse']:.2f} ms", flush=True)
+    rt = ""
+    if len(sys.argv) > 3 and sys.argv[3] == "check":  # round trip at this size (host buffers)
+        f = zk.forward_fft(sg, pts)
+        rt = ", round trip " + ("exact" if np.array_equal(zk.inverse_fft(sg, f), pts) else "MISMATCH")
+    print(f"{curve} 2^{m} group FFT: forward {out['forward']:.2f} ms, inverse {out['inverse']:.2f} ms (glv {glv}){rt}",
+          flush=True)

@@ -1,10 +1,9 @@
-# r04k: window sweep for 2^17..2^19 (the Y sums cost the same 0.32 ms at c = 16 from 2^18 to 2^20)
+# r04n: GLV group FFT after the window-offset fix; bits-path timeline and phases
 cd "$GRAFT_REPO_ROOT"
-for rep in 1 2; do
-  for lg in 17 18 19 20; do
-    timeout -k 10 200 python -u tools/sweep_window.py bls12_381 $lg 13 14 15 16 2>&1 | grep -v amdgpu.ids || exit 1
-  done
-  for lg in 17 18 19 20; do
-    timeout -k 10 200 python -u tools/sweep_window.py bn128 $lg 13 14 15 16 2>&1 | grep -v amdgpu.ids || exit 1
-  done
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_g1ext.py tests/test_gpu_msm_bits.py -m gpu 2>&1 | tail -15 || exit 1
+timeout -k 10 300 python -u tools/fft_time.py 16 3 check 2>&1 | grep -v amdgpu.ids || exit 1
+for lg in 10 12; do
+  ZK_PROBE_PHASES=1 timeout -k 10 120 python -u tools/small_probe.py bls12_381 $lg 20 2>&1 | grep -v amdgpu.ids || exit 1
 done
+timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/r04n_tr10 -o run --output-format csv -- python3 tools/small_probe.py bls12_381 10 6 > gpurun_out/r04n_tr10.log 2>&1 || exit 1

@@ -18,8 +18,13 @@ for m in ms:
                m.get("Stream_Id", "")))
 ev.sort()
 starts, prev = [], None
+idle = len(sys.argv) > 2 and sys.argv[2] == "idle"  # calls separated by >= 1 ms with nothing running
 for i, e in enumerate(ev):
-    if e[2] == "C" and e[3].startswith("HOST_TO_DEVICE"):
+    if idle:
+        if prev is None or e[0] - prev > 1_000_000:
+            starts.append(i)
+        prev = e[1] if prev is None else max(prev, e[1])
+    elif e[2] == "C" and e[3].startswith("HOST_TO_DEVICE"):
         if prev is None or e[0] - prev > 1_000_000:
             starts.append(i)
         prev = e[1]

@@ -45,6 +45,8 @@ void fft_g(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t 
 }
 }  // namespace
 
+ZKG_API int zkg_g1_fft_last_glv(void) { return zk::g1_fft_last_glv().load(); }
+
 namespace {
 const uint64_t kZero[4] = {0, 0, 0, 0};
 template <class Fh>

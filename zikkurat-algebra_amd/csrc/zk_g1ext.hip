@@ -402,6 +402,402 @@ __device__ __forceinline__ void xyzz_scl(Xyzz<F> &r, const Xyzz<F> &P, const uin
   fe_mul(r.ZZZ, r.ZZ, acc.Z);
 }
 
+// ---------------------------------------------------------------------------- GLV stages
+// On the order-r subgroup phi(x, y) = (beta x, y) is [lambda], so k P = k1 P + k2 phi(P) with
+// |k1|, |k2| < 2^130 (k = k1 + k2 lambda mod r; constants: zk_glv.inc, tools/gen_glv.py).  A
+// butterfly's multiplication then runs on a PAIR of lanes -- lane 0: k1 P, lane 1: k2 phi(P), 27
+// signed 5-bit windows (130 doublings) each -- and the pair swaps results (DPP) and adds them.
+// The chain per lane is ~half of the 255-doubling one, and the stage has twice the lanes (2^16
+// points: 2^16 lanes instead of 2^15, so every SIMD holds a wavefront).  Valid only on the
+// subgroup (for other points k P depends on the integer k, not on k mod r, and the reference
+// multiplies by the integer): BN254 G1 has cofactor 1; BLS12-381 inputs are checked first
+// (k_subgroup_check) and the call falls back to the integer stages when any point fails.
+#include "zk_glv.inc"
+
+struct GlvParams {  // decomposition constants of one curve (kernel argument)
+  uint64_t g1[4], g2[4], a1[3], b1[3], a2[3], b2[3], lambda[3];
+  int s1, s2;
+};
+template <class C>
+static GlvParams glv_params() {
+  GlvParams p;
+  auto cp = [](uint64_t *d, const uint64_t *s, int n) { for (int i = 0; i < n; i++) d[i] = s[i]; };
+  if constexpr (C::NP64 == 4) {
+    cp(p.g1, GLV_BN254_G1, 4); cp(p.g2, GLV_BN254_G2, 4);
+    cp(p.a1, GLV_BN254_A1, 3); cp(p.b1, GLV_BN254_B1, 3); cp(p.a2, GLV_BN254_A2, 3); cp(p.b2, GLV_BN254_B2, 3);
+    cp(p.lambda, GLV_BN254_LAMBDA, 3);
+    p.s1 = GLV_BN254_SGN1; p.s2 = GLV_BN254_SGN2;
+  } else {
+    cp(p.g1, GLV_BLS381_G1, 4); cp(p.g2, GLV_BLS381_G2, 4);
+    cp(p.a1, GLV_BLS381_A1, 3); cp(p.b1, GLV_BLS381_B1, 3); cp(p.a2, GLV_BLS381_A2, 3); cp(p.b2, GLV_BLS381_B2, 3);
+    cp(p.lambda, GLV_BLS381_LAMBDA, 3);
+    p.s1 = GLV_BLS381_SGN1; p.s2 = GLV_BLS381_SGN2;
+  }
+  return p;
+}
+template <class C>
+static W6 glv_beta_ref() {
+  W6 b = {{0, 0, 0, 0, 0, 0}};
+  const uint64_t *s = C::NP64 == 4 ? GLV_BN254_BETA_REF : GLV_BLS381_BETA_REF;
+  for (int i = 0; i < C::NP64; i++) b.w[i] = s[i];
+  return b;
+}
+
+// 192-bit two's complement helpers (values of the decomposition are < 2^131 in magnitude)
+__device__ __forceinline__ void u192_mul(uint64_t r[3], const uint64_t a[3], const uint64_t b[3]) {
+  const uint64_t lo00 = a[0] * b[0], hi00 = __umul64hi(a[0], b[0]);
+  const uint64_t lo01 = a[0] * b[1], hi01 = __umul64hi(a[0], b[1]);
+  const uint64_t lo10 = a[1] * b[0], hi10 = __umul64hi(a[1], b[0]);
+  r[0] = lo00;
+  const uint64_t s1 = hi00 + lo01, c1 = s1 < hi00 ? 1 : 0;
+  const uint64_t s2 = s1 + lo10, c2 = s2 < s1 ? 1 : 0;
+  r[1] = s2;
+  r[2] = hi01 + hi10 + c1 + c2 + a[0] * b[2] + a[1] * b[1] + a[2] * b[0];
+}
+__device__ __forceinline__ void u192_sub(uint64_t r[3], const uint64_t a[3], const uint64_t b[3]) {
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const uint64_t d = a[i] - b[i], b1 = a[i] < b[i] ? 1 : 0, d2 = d - br, b2 = d < br ? 1 : 0;
+    r[i] = d2;
+    br = b1 | b2;
+  }
+}
+__device__ __forceinline__ void u192_neg(uint64_t r[3], const uint64_t a[3]) {
+  const uint64_t z[3] = {0, 0, 0};
+  u192_sub(r, z, a);
+}
+// c = floor(k g / 2^382) (k, g < 2^256; c < 2^130)
+__device__ __forceinline__ void glv_round(uint64_t c[3], const uint64_t k[4], const uint64_t g[4]) {
+  uint64_t p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint64_t lo = k[i] * g[j], hi = __umul64hi(k[i], g[j]);
+      const uint64_t s = p[i + j] + lo, c1 = s < lo ? 1 : 0;
+      const uint64_t s2 = s + carry, c2 = s2 < s ? 1 : 0;
+      p[i + j] = s2;
+      carry = hi + c1 + c2;
+    }
+    p[i + 4] = carry;
+  }
+  c[0] = (p[5] >> 62) | (p[6] << 2);
+  c[1] = (p[6] >> 62) | (p[7] << 2);
+  c[2] = p[7] >> 62;
+}
+// k (standard form, < r) -> |k1|, |k2| (3 words each) and their signs (bit 0: k1 < 0, bit 1: k2 < 0)
+__device__ __forceinline__ void glv_decompose(uint64_t out[8], const uint64_t k[4], const GlvParams &P) {
+  uint64_t c1[3], c2[3], t[3], k1[3], k2[3];
+  glv_round(c1, k, P.g1);
+  glv_round(c2, k, P.g2);
+  if (P.s1 < 0) u192_neg(c1, c1);
+  if (P.s2 < 0) u192_neg(c2, c2);
+  const uint64_t kk[3] = {k[0], k[1], k[2]};
+  u192_mul(t, c1, P.a1);
+  u192_sub(k1, kk, t);
+  u192_mul(t, c2, P.a2);
+  u192_sub(k1, k1, t);  // k1 = k - c1 a1 - c2 a2
+  u192_mul(t, c1, P.b1);
+  u192_neg(k2, t);
+  u192_mul(t, c2, P.b2);
+  u192_sub(k2, k2, t);  // k2 = -c1 b1 - c2 b2
+  uint32_t sg = 0;
+  if (k1[2] >> 63) { u192_neg(k1, k1); sg |= 1; }
+  if (k2[2] >> 63) { u192_neg(k2, k2); sg |= 2; }
+  out[0] = k1[0]; out[1] = k1[1]; out[2] = k1[2];
+  out[3] = k2[0]; out[4] = k2[1]; out[5] = k2[2];
+  out[6] = sg;
+  out[7] = 0;
+}
+
+// twg[e] = GLV decomposition of std(scale * base^e) (8 u64 per entry), e < cnt
+template <class Fr>
+__global__ void __launch_bounds__(256) k_fft_tw_glv(int cnt, W6 base, W6 scale, GlvParams gp,
+                                                    uint64_t *__restrict__ twg) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= cnt) return;
+  Fe<Fr> b, acc, t;
+  ld_int(b, base.w);
+  fe_load_ref(acc, scale.w);
+  Fe<Fr> p = b;
+  for (int x = e; x; x >>= 1) {
+    if (x & 1) { fe_mul(t, acc, p); acc = t; }
+    fe_sqr(t, p);
+    p = t;
+  }
+  Fe<Fr> sd;
+  fe_ref_to_std(sd, acc);
+  uint64_t k[4], o[8];
+  fe_store_ref(k, sd);
+  glv_decompose(o, k, gp);
+#pragma unroll
+  for (int i = 0; i < 8; i++) twg[(size_t)e * 8 + i] = o[i];
+}
+
+// point-pair swap inside a lane pair (DPP quad_perm [1, 0, 3, 2])
+template <class F>
+__device__ __forceinline__ void fe_pair_swap(Fe<F> &r, const Fe<F> &v) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.v[i], 0xB1, 0xf, 0xf, false);
+}
+template <class F>
+__device__ __forceinline__ void xyzz_to_jac(Jac<F> &p, const Xyzz<F> &P) {  // P not infinity
+  Fe<F> z2, z4, t;
+  fe_sqr(z2, P.ZZZ);
+  fe_mul(t, P.X, P.ZZ);
+  fe_mul(p.X, t, z2);
+  fe_sqr(z4, z2);
+  fe_mul(p.Y, P.Y, z4);
+  fe_mul(p.Z, P.ZZ, P.ZZZ);
+}
+template <class F>
+__device__ __forceinline__ void jac_to_xyzz(Xyzz<F> &r, const Jac<F> &a) {
+  if (jac_is_inf(a)) {
+    xyzz_set_inf(r);
+    return;
+  }
+  r.X = a.X;
+  r.Y = a.Y;
+  fe_sqr(r.ZZ, a.Z);
+  fe_mul(r.ZZZ, r.ZZ, a.Z);
+}
+// acc += b, either may be infinity
+template <class F>
+__device__ __forceinline__ void jac_add_any(Jac<F> &acc, const Jac<F> &b) {
+  if (jac_is_inf(b)) return;
+  if (jac_is_inf(acc)) {
+    acc = b;
+    return;
+  }
+  JacC<F> c;
+  jac_cache(c, b);
+  jac_add_cached(acc, c);
+}
+// window i (5 bits) of a 3-word K
+__device__ __forceinline__ uint32_t win5_3(const uint64_t *K, int i) {
+  const int b = 5 * i, w = b >> 6, o = b & 63;
+  uint64_t v = K[w] >> o;
+  if (o > 59 && w < 2) v |= K[w + 1] << (64 - o);
+  return (uint32_t)v & 31u;
+}
+// r = k p for k < 2^130 (3 words), p finite: 16-entry table, 27 signed 5-bit windows
+// (K = k + 16 sum_{i<27} 32^i < 2^135)
+template <class F>
+__device__ __forceinline__ void jac_scl130(Jac<F> &acc, const Jac<F> &p, const uint64_t *k, uint32_t *__restrict__ tab) {
+  {
+    Jac<F> a;
+    JacC<F> pc, c;
+    jac_cache(pc, p);
+    jacc_store(tab, pc);
+    a = p;
+    jac_dbl(a);
+    jac_cache(c, a);
+    jacc_store(tab + 1 * 5 * F::SN, c);
+    for (int d = 3; d <= SCL_TAB; d++) {
+      jac_add_cached(a, pc);
+      jac_cache(c, a);
+      jacc_store(tab + (size_t)(d - 1) * 5 * F::SN, c);
+    }
+  }
+  uint64_t K[3];
+  {
+    const uint64_t H[3] = {0x0842108421084210ull, 0x1084210842108421ull, 0x0000000000000042ull};
+    uint64_t cy = 0;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const uint64_t a = k[j], s1 = a + H[j];
+      const uint64_t c1 = s1 < a ? 1 : 0, s2 = s1 + cy;
+      K[j] = s2;
+      cy = c1 | (s2 < s1 ? 1 : 0);
+    }
+  }
+  fe_one(acc.X);
+  fe_one(acc.Y);
+  fe_zero(acc.Z);
+  for (int i = 26; i >= 0; i--) {
+    if (i != 26)
+      for (int z = 0; z < 5; z++) jac_dbl(acc);
+    const int d = (int)win5_3(K, i) - 16;
+    if (d) {
+      JacC<F> e;
+      jacc_load(e, tab + (size_t)((d < 0 ? -d : d) - 1) * 5 * F::SN);
+      if (d < 0) {
+        Fe<F> ny;
+        fe_neg(ny, e.Y);
+        e.Y = ny;
+      }
+      jac_add_cached(acc, e);
+    }
+  }
+}
+// pair-cooperative t = k v (k decomposed: dk = |k1|, |k2|, signs): lane q of the pair computes
+// its half, the pair swaps and adds (both lanes end with t)
+template <class F>
+__device__ __forceinline__ void glv_scl_pair(Xyzz<F> &t, const Xyzz<F> &v, const uint64_t *__restrict__ dk,
+                                             const Fe<F> &beta, uint32_t *__restrict__ tab) {
+  const int q = (int)(threadIdx.x & 1);
+  Jac<F> r;
+  if (xyzz_is_inf(v)) {
+    fe_one(r.X);
+    fe_one(r.Y);
+    fe_zero(r.Z);
+  } else {
+    Jac<F> p;
+    xyzz_to_jac(p, v);
+    if (q) {
+      Fe<F> bx;
+      fe_mul(bx, p.X, beta);
+      p.X = bx;
+    }
+    if ((dk[6] >> q) & 1) {
+      Fe<F> ny;
+      fe_neg(ny, p.Y);
+      p.Y = ny;
+    }
+    jac_scl130(r, p, dk + 3 * q, tab);
+  }
+  Jac<F> o;
+  fe_pair_swap(o.X, r.X);
+  fe_pair_swap(o.Y, r.Y);
+  fe_pair_swap(o.Z, r.Z);
+  jac_add_any(r, o);
+  jac_to_xyzz(t, r);
+}
+
+// forward DIT stage on lane pairs: pair = butterfly; lane 0 writes u + t, lane 1 u - t
+template <class C>
+__global__ void __launch_bounds__(256) k_fft_fwd_stage_glv(int m, int s, const uint32_t *__restrict__ A,
+                                                           uint32_t *__restrict__ B, const uint64_t *__restrict__ twg,
+                                                           W6 beta_ref, uint32_t *__restrict__ scratch, int lanes) {
+  using F = typename C::Fp;
+  const int half = 1 << (s - 1);
+  const size_t nl = (size_t)1 << m;  // two lanes per butterfly
+  Fe<F> beta, t0;
+  fe_load_ref(t0, beta_ref.w);
+  fe_to_int(beta, t0);
+  uint32_t *tab = scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>();
+  for (size_t L = (size_t)blockIdx.x * blockDim.x + threadIdx.x; L < nl; L += (size_t)lanes) {
+    const size_t b = L >> 1;
+    const int q = (int)(L & 1);
+    const size_t blk = b >> (s - 1), j = b & (half - 1);
+    const size_t k0 = (blk << s) + j;
+    Xyzz<F> u, v, t;
+    xyzz_load(u, A + k0 * xw<F>());
+    xyzz_load(v, A + (k0 + half) * xw<F>());
+    if (j == 0) t = v;
+    else glv_scl_pair(t, v, twg + (j << (m - s)) * 8, beta, tab);
+    if (q) {
+      Xyzz<F> nt;
+      xyzz_neg(nt, t);
+      t = nt;
+    }
+    xyzz_add(u, t);
+    xyzz_store(B + (k0 + (q ? half : 0)) * xw<F>(), u);
+  }
+}
+
+// inverse DIF stage on lane pairs, factor 1/2 per level deferred (k_fft_scale_glv applies N^-1
+// once): lane 0 writes u + v, lane 1 (u - v) w^-j
+template <class C>
+__global__ void __launch_bounds__(256) k_fft_inv_stage_glv(int m, int s, const uint32_t *__restrict__ A,
+                                                           uint32_t *__restrict__ B, const uint64_t *__restrict__ twg,
+                                                           W6 beta_ref, uint32_t *__restrict__ scratch, int lanes) {
+  using F = typename C::Fp;
+  const int half = 1 << (s - 1);
+  const size_t nl = (size_t)1 << m;
+  Fe<F> beta, t0;
+  fe_load_ref(t0, beta_ref.w);
+  fe_to_int(beta, t0);
+  uint32_t *tab = scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>();
+  for (size_t L = (size_t)blockIdx.x * blockDim.x + threadIdx.x; L < nl; L += (size_t)lanes) {
+    const size_t b = L >> 1;
+    const int q = (int)(L & 1);
+    const size_t blk = b >> (s - 1), j = b & (half - 1);
+    const size_t k0 = (blk << s) + j;
+    Xyzz<F> u, v, d;
+    xyzz_load(u, A + k0 * xw<F>());
+    xyzz_load(v, A + (k0 + half) * xw<F>());
+    d = u;
+    {
+      Xyzz<F> nv;
+      xyzz_neg(nv, v);
+      xyzz_add(d, nv);
+    }
+    Xyzz<F> t = d;
+    if (j != 0) glv_scl_pair(t, d, twg + (j << (m - s)) * 8, beta, tab);
+    if (q == 0) {
+      xyzz_add(u, v);
+      t = u;
+    }
+    xyzz_store(B + (k0 + (q ? half : 0)) * xw<F>(), t);
+  }
+}
+
+// every point times one decomposed scalar dk (the inverse's N^-1), lane pairs
+template <class C>
+__global__ void __launch_bounds__(256) k_fft_scale_glv(int n, const uint32_t *__restrict__ A, uint32_t *__restrict__ B,
+                                                       const uint64_t *__restrict__ dk, W6 beta_ref,
+                                                       uint32_t *__restrict__ scratch, int lanes) {
+  using F = typename C::Fp;
+  Fe<F> beta, t0;
+  fe_load_ref(t0, beta_ref.w);
+  fe_to_int(beta, t0);
+  uint32_t *tab = scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>();
+  for (size_t L = (size_t)blockIdx.x * blockDim.x + threadIdx.x; L < 2 * (size_t)n; L += (size_t)lanes) {
+    const size_t i = L >> 1;
+    Xyzz<F> v, t;
+    xyzz_load(v, A + i * xw<F>());
+    glv_scl_pair(t, v, dk, beta, tab);
+    if ((L & 1) == 0) xyzz_store(B + i * xw<F>(), t);
+  }
+}
+
+// subgroup membership (curves with a cofactor): phi(P) == [lambda] P for every point (lambda
+// 128 bits on BLS12-381; tools/gen_glv.py checks the test on subgroup and non-subgroup points).
+// bad[block] = 1 when some point of the block fails.
+template <class C>
+__global__ void __launch_bounds__(256) k_subgroup_check(int n, const uint32_t *__restrict__ A, GlvParams gp,
+                                                        W6 beta_ref, uint32_t *__restrict__ scratch, int lanes,
+                                                        uint32_t *__restrict__ bad) {
+  using F = typename C::Fp;
+  Fe<F> beta, t0;
+  fe_load_ref(t0, beta_ref.w);
+  fe_to_int(beta, t0);
+  uint32_t *tab = scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>();
+  int fail = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += (size_t)lanes) {
+    Xyzz<F> v;
+    xyzz_load(v, A + i * xw<F>());
+    if (xyzz_is_inf(v)) continue;
+    Jac<F> p, r;
+    xyzz_to_jac(p, v);
+    jac_scl130(r, p, gp.lambda, tab);
+    if (jac_is_inf(r)) {
+      fail = 1;
+      continue;
+    }
+    // (beta Xp : Yp : Zp) == (Xr : Yr : Zr): Xr Zp^2 == beta Xp Zr^2 and Yr Zp^3 == Yp Zr^3
+    Fe<F> zp2, zr2, zp3, zr3, a, b, c;
+    fe_sqr(zp2, p.Z);
+    fe_sqr(zr2, r.Z);
+    fe_mul(zp3, zp2, p.Z);
+    fe_mul(zr3, zr2, r.Z);
+    fe_mul(a, r.X, zp2);
+    fe_mul(c, p.X, beta);
+    fe_mul(b, c, zr2);
+    fe_sub(c, a, b);
+    if (!fe_is_zero(c)) fail = 1;
+    fe_mul(a, r.Y, zp3);
+    fe_mul(b, p.Y, zr3);
+    fe_sub(c, a, b);
+    if (!fe_is_zero(c)) fail = 1;
+  }
+  const int any = __syncthreads_or(fail);
+  if (threadIdx.x == 0) bad[blockIdx.x] = any ? 1u : 0u;
+}
+
 // forward DIT stage s (block 2^s): lane = butterfly (blk, j); t = w_s^j v (w_s^j = tw[j 2^(m-s)],
 // canonical Fr in standard form, = 1 for j = 0); out = (u + t, u - t)
 template <class C>
@@ -573,8 +969,14 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   lanes = (lanes + 255) & ~(size_t)255;
   if (lanes == 0) lanes = 256;
   const size_t tw_cnt = N > 1 ? N / 2 : 1;
-  dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 2 * N * xw<F>() * 4 + lanes * scl_tab_words<F>() * 4 +
-                    tw_cnt * 32 + N * NP * 8 + (1 << 20));
+  // GLV stages: two lanes per multiplication (forward N / 2 butterflies, inverse N / 2 plus the
+  // final N^-1 scaling of N points)
+  size_t glanes = N < (1u << 17) ? N : (1u << 17);
+  glanes = (glanes + 255) & ~(size_t)255;
+  const size_t tlanes = std::max(lanes, glanes);
+  const size_t nbad = div_up(N, 256);
+  dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 2 * N * xw<F>() * 4 + tlanes * scl_tab_words<F>() * 4 +
+                    tw_cnt * 32 + tw_cnt * 64 + 64 + nbad * 4 + N * NP * 8 + (1 << 20));
   dev.arena.reset();
   const uint64_t *ds = src;
   uint64_t *dt = tgt;
@@ -586,13 +988,73 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   }
   uint32_t *A = dev.arena.take<uint32_t>(N * xw<F>());
   uint32_t *B = dev.arena.take<uint32_t>(N * xw<F>());
-  uint32_t *scratch = dev.arena.take<uint32_t>(lanes * scl_tab_words<F>());
+  uint32_t *scratch = dev.arena.take<uint32_t>(tlanes * scl_tab_words<F>());
   uint64_t *tw = dev.arena.take<uint64_t>(tw_cnt * 4);
+  uint64_t *twg = dev.arena.take<uint64_t>(tw_cnt * 8 + 8);
+  uint32_t *bad = dev.arena.take<uint32_t>(nbad);
   uint64_t *nscratch = dev.arena.take<uint64_t>(N * NP);
 
   hipLaunchKernelGGL(k_fft_load<C>, dim3(div_up(N, 256)), dim3(256), 0, st, (int)N, inverse ? 0 : m, ds, A);
   ZK_CHECK(hipGetLastError());
-  if (m > 0) {
+  // GLV stages when every point is in the order-r subgroup (always on BN254, cofactor 1; checked
+  // on BLS12-381).  ZK_FFT_GLV=0: the integer stages always (A/B hook, read once).
+  static const bool glv_on = [] {
+    const char *e = getenv("ZK_FFT_GLV");
+    return !(e && e[0] == '0');
+  }();
+  bool glv = glv_on && m > 0;
+  const GlvParams gp = glv_params<C>();
+  const W6 beta = glv_beta_ref<C>();
+  if (glv && C::NP64 == 6) {
+    const unsigned grid = (unsigned)(glanes / 256);
+    hipLaunchKernelGGL(k_subgroup_check<C>, dim3(grid), dim3(256), 0, st, (int)N, A, gp, beta, scratch, (int)glanes,
+                       bad);
+    ZK_CHECK(hipGetLastError());
+    uint32_t *hb = reinterpret_cast<uint32_t *>(dev.host_staging(grid * 4 + 64));
+    ZK_CHECK(hipMemcpyAsync(hb, bad, grid * 4, hipMemcpyDeviceToHost, st));
+    ZK_CHECK(hipStreamSynchronize(st));
+    for (unsigned i = 0; i < grid; i++) glv = glv && hb[i] == 0;
+  }
+  g1_fft_last_glv().store(glv ? 1 : 0);
+  if (glv) {
+    // twiddles (decomposed): forward w^e; inverse (w^-1)^e with the 1/2 per level deferred to one
+    // final multiplication by N^-1 (on the subgroup ((u + v) / 2 ...) over m levels = N^-1 (...))
+    zkh::Fe<HR> g, one, ninv;
+    memcpy(g.v, gen, sizeof g.v);
+    zkh::set_one(one);
+    if (inverse) zkh::inv(g, g);
+    W6 wb = {{0, 0, 0, 0, 0, 0}}, ws = {{0, 0, 0, 0, 0, 0}}, wn = {{0, 0, 0, 0, 0, 0}};
+    for (int j = 0; j < 4; j++) { wb.w[j] = g.v[j]; ws.w[j] = one.v[j]; }
+    hipLaunchKernelGGL(k_fft_tw_glv<Fr>, dim3(div_up(tw_cnt, 256)), dim3(256), 0, st, (int)tw_cnt, wb, ws, gp, twg);
+    ZK_CHECK(hipGetLastError());
+    const unsigned grid = (unsigned)(glanes / 256);
+    uint32_t *in = A, *out = B;
+    for (int k = 0; k < m; k++) {
+      const int s = inverse ? m - k : k + 1;
+      if (inverse)
+        hipLaunchKernelGGL(k_fft_inv_stage_glv<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, twg, beta, scratch,
+                           (int)glanes);
+      else
+        hipLaunchKernelGGL(k_fft_fwd_stage_glv<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, twg, beta, scratch,
+                           (int)glanes);
+      ZK_CHECK(hipGetLastError());
+      std::swap(in, out);
+    }
+    if (inverse) {  // N^-1, decomposed like a twiddle (entry 0 of a one-entry table)
+      zkh::Fe<HR> nn = one;
+      for (int k = 0; k < m; k++) zkh::add(nn, nn, nn);
+      zkh::inv(ninv, nn);
+      for (int j = 0; j < 4; j++) wn.w[j] = ninv.v[j];
+      uint64_t *dk = twg + tw_cnt * 8;
+      hipLaunchKernelGGL(k_fft_tw_glv<Fr>, dim3(1), dim3(256), 0, st, 1, wb, wn, gp, dk);
+      ZK_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(k_fft_scale_glv<C>, dim3(grid), dim3(256), 0, st, (int)N, in, out, dk, beta, scratch,
+                         (int)glanes);
+      ZK_CHECK(hipGetLastError());
+      std::swap(in, out);
+    }
+    A = in;
+  } else if (m > 0) {
     // twiddles: forward w^e; inverse (w^-1)^e / 2 -- the reference's gpow sequences
     // (G1_proj.c:705-711, 758-764), canonical Fr, standard form
     zkh::Fe<HR> g, scale;

@@ -1,6 +1,7 @@
 // zk_g1ext.hpp -- C++ interface of the G1 batch conversions and the group FFT (zk_g1ext.hip)
 #pragma once
 #include <stdint.h>
+#include <atomic>
 
 namespace zk {
 
@@ -10,5 +11,10 @@ void g1_batch_from_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, 
 void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io);
 // group FFT of 2^m projective points with Fr generator `gen` (host, Montgomery); outputs normalised
 void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse);
+// 1 when the most recent group FFT ran the GLV stages (test / bench probe)
+inline std::atomic<int> &g1_fft_last_glv() {
+  static std::atomic<int> v{0};
+  return v;
+}
 
 }  // namespace zk

@@ -1147,6 +1147,94 @@ __global__ void __launch_bounds__(256) k_jobsum_blk(const uint32_t *__restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Small inputs: bit jobs straight on the pairs, no buckets.
+//   sum_i k_i P_i = sum_t 2^t Q_t,   Q_t = sum of the P_i whose scalar has bit t set
+// Every step of the bucket pipeline is latency-bound at a few thousand pairs (a lone lane's
+// point operation ~8 us, ~25 of them in a row through sort, accumulation, stitch, Y sums and
+// job sums: BLS12-381 2^10 spent 0.38 ms on the device, profiles/r04l_*).  Here the chain is
+// K = n / G mixed additions per lane plus a log-depth quad fold, and the host runs the usual
+// Horner over the bits (its chain of ~255 doublings is the same as after the bucket pipeline).
+// The work is nbits n predicated mixed additions -- 8-9x the bucket method's W n -- so the
+// path only pays below a few thousand pairs (msm_bits_max).
+//
+// k_bitacc: block g = pairs [g K, g K + K), thread t = bit t (a wavefront covers 64 bits, so the
+// point of step e is one uniform load for the whole block).  The K scalars are converted to
+// integers (REDC when Montgomery) into LDS first; lane t adds P_e when bit t of k_e is set.
+// Output: partial sum of bit t over the chunk at part[t G + g] (lazy XYZZ, like k_accum's flushes).
+template <class C>
+__global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
+    k_bitacc(const uint64_t *__restrict__ scalars, int n, int stride, int loff, int nread, int mont, int nbits, int K,
+             const uint32_t *__restrict__ points, uint32_t *__restrict__ part) {
+  using F = typename C::Fp;
+  constexpr int AW = aff_words<F>();
+  __shared__ uint32_t sk[256][9];  // integer scalars of the chunk (8 words, padded)
+  const int t = threadIdx.x, g = blockIdx.x, G = gridDim.x;
+  const int p0 = g * K, np = min(K, n - p0);
+  for (int e = t; e < np; e += 256) {
+    DigitStream<C> ds;
+    ds.load(scalars, p0 + e, stride, loff, nread, mont);
+#pragma unroll
+    for (int j = 0; j < 8; j++) sk[e][j] = ds.k[j];
+  }
+  __syncthreads();
+  if (t >= nbits) return;
+  const int word = t >> 5;
+  const uint32_t bit = (uint32_t)t & 31u;
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  for (int e = 0; e < np; e++) {
+    if ((sk[e][word] >> bit) & 1u) {
+      Aff<F> P;
+      if (aff_load(P, points + (size_t)(p0 + e) * AW)) xyzz_acc_aff(acc, P);
+    }
+  }
+  xyzz_store(part + ((size_t)t * G + g) * xyzz_words<F>(), acc);
+}
+
+// k_bitsum: one 256-thread block per bit t = 64 quad lanes (xyzz_add_quad): quad q adds the
+// partials q, q + 64, ... of row t, then the block folds the active quads through LDS (depth
+// log2 min(G, 64)); exports Q_t in the canonical reference form (X, Y, ZZ, ZZZ) for the host.
+template <class C>
+__global__ void __launch_bounds__(256) k_bitsum(const uint32_t *__restrict__ part, int G, uint64_t *__restrict__ out) {
+  using F = typename C::Fp;
+  constexpr int XW = xyzz_words<F>();
+  __shared__ uint32_t park_lds[256 * XW];  // xyzz_add_quad's doubling fallback, per lane
+  __shared__ uint4 fold4[32 * XW / 4];     // fold exchange, one slot per upper-half quad
+  uint32_t *fold = reinterpret_cast<uint32_t *>(fold4);
+  uint32_t *park = park_lds + threadIdx.x * XW;
+  const int tb = blockIdx.x;
+  const int q = threadIdx.x >> 2;  // quad (logical lane) 0..63
+  const uint32_t *row = part + (size_t)tb * G * XW;
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  for (int e = q; e < G; e += 64) {
+    Xyzz<F> p;
+    xyzz_load(p, row + (size_t)e * XW);
+    xyzz_add_quad(acc, p, park);
+  }
+  const int act = G < 64 ? G : 64;
+  int h0 = 1;
+  while (2 * h0 < act) h0 <<= 1;
+  for (int h = act > 1 ? h0 : 0; h >= 1; h >>= 1) {
+    if (q >= h && q < 2 * h && (threadIdx.x & 3) == 0) xyzz_store(fold + (size_t)(q - h) * XW, acc);
+    __syncthreads();
+    if (q < h) {
+      Xyzz<F> o;
+      xyzz_load(o, fold + (size_t)q * XW);
+      xyzz_add_quad(acc, o, park);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) {
+    const int l = (int)threadIdx.x;
+    Fe<F> v, r;
+    fe_sel4(v, acc.X, acc.Y, acc.ZZ, acc.ZZZ, l);
+    fe_to_ref(r, v);
+    fe_store_ref(out + ((size_t)tb * 4 + l) * C::NP64, r);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host orchestration
 
 struct MsmShape {
@@ -1675,11 +1763,14 @@ struct GroupPass {
 // thread runs the cross-window chain of c (W - 1) doublings (Jacobian, 2M + 5S each),
 // waiting for each V_w only when the chain reaches it.  On one host core a point op costs
 // ~0.4 us against ~20 us for a lone GPU lane, which is why this tail stays on the host.
+// bits > 0: the small-input layout instead (k_bitsum): `bits` sums Q_t, t = 0 .. bits-1, in
+// windows of c: job j of window w is Q_{c w + j} with exponent j.
 template <class C>
-static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typename HostOf<C>::Fp> &out) {
+static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typename HostOf<C>::Fp> &out,
+                        int bits = 0) {
   using HF = typename HostOf<C>::Fp;
   const int NP = C::NP64;
-  const int J = c, E = c - 1;  // local exponents 0 .. c-2
+  const int J = c, E = bits ? c : c - 1;  // local exponents 0 .. E-1
   std::vector<zkh::Jac<HF>> V(W);
   std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[W]);
   for (int w = 0; w < W; w++) ready[w].store(0, std::memory_order_relaxed);
@@ -1688,6 +1779,7 @@ static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typena
     std::vector<zkh::Xyzz<HF>> Z(E);
     for (auto &z : Z) zkh::xyzz_set_inf(z);
     for (int j = 0; j < J; j++) {
+      if (bits && c * w + j >= bits) break;
       const uint64_t *q = exported + ((size_t)w * J + j) * 4 * NP;
       zkh::Xyzz<HF> p;
       memcpy(p.X.v, q + 0 * NP, NP * 8);
@@ -1695,7 +1787,7 @@ static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typena
       memcpy(p.ZZ.v, q + 2 * NP, NP * 8);
       memcpy(p.ZZZ.v, q + 3 * NP, NP * 8);
       if (zkh::xyzz_is_inf(p)) continue;
-      const int e = j == 0 ? 0 : j - 1;
+      const int e = bits ? j : (j == 0 ? 0 : j - 1);
       zkh::xyzz_add(Z[e], Z[e], p);
     }
     zkh::Xyzz<HF> acc;
@@ -1720,6 +1812,90 @@ static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typena
   zkh::jac_to_xyzz(out, acc);
 }
 
+// Largest n that takes the bit-job path (default-window calls).  ZK_MSM_BITS_MAX overrides it
+// (experiment / A-B hook, read once; 0 = always the bucket pipeline).
+#ifndef ZK_MSM_BITS_MAX
+#define ZK_MSM_BITS_MAX 4096
+#endif
+inline int msm_bits_max() {
+  static const int v = [] {
+    const char *e = getenv("ZK_MSM_BITS_MAX");
+    return e ? atoi(e) : ZK_MSM_BITS_MAX;
+  }();
+  return v;
+}
+// chunks of the bit-job accumulation: ~256 blocks (one wavefront per SIMD for the 4 x 64 bits)
+// so a lane's chain is K = n / 256 mixed additions; ZK_MSM_BITS_G overrides the block count
+inline int msm_bits_groups(int n) {
+  static const int g = [] {
+    const char *e = getenv("ZK_MSM_BITS_G");
+    const int v = e ? atoi(e) : 256;
+    return v >= 1 ? v : 256;
+  }();
+  const int K = (n + g - 1) / g;
+  return (n + K - 1) / K;
+}
+
+// The small-input path (k_bitacc / k_bitsum above): points to internal form, bit-job partial
+// sums, per-bit sums exported to the host, Horner over the bits in windows of 8 on the host.
+template <class C>
+static void msm_run_bits(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t *points, bool host_inputs,
+                         int nbits, zkh::Xyzz<typename HostOf<C>::Fp> &out) {
+  using F = typename C::Fp;
+  constexpr int XW = xyzz_words<F>();
+  ZK_REQUIRE(nbits >= 1 && nbits <= 256, "msm: bit-job path takes at most 256-bit scalars (internal)");
+  const int G = msm_bits_groups(n), K = (n + G - 1) / G;
+  hipStream_t st = dev.stream;
+  const size_t sc_bytes = host_inputs ? (size_t)n * sc_in.stride * 8 : 0;
+  const size_t pt_bytes = host_inputs ? (size_t)n * 2 * C::NP64 * 8 : 0;
+  const size_t int_bytes = (size_t)n * aff_words<F>() * 4;
+  const size_t part_bytes = (size_t)nbits * G * XW * 4;
+  const size_t exp_bytes = (size_t)nbits * 4 * C::NP64 * 8;
+  const size_t need = sc_bytes + pt_bytes + int_bytes + part_bytes + exp_bytes + 5 * 256;
+  if (!dev.arena.try_reserve(need)) {
+    ZK_CHECK(hipStreamSynchronize(st));
+    ntt_release(dev);
+    ZK_REQUIRE(dev.arena.try_reserve(need), "msm: out of device memory");
+  }
+  dev.arena.reset();
+  msm_last_groups().store(1);
+  PhaseProf prof(st);
+  ScalarSlice sc = sc_in;
+  const uint64_t *pts_ref = points;
+  if (host_inputs) {
+    uint64_t *a = dev.arena.take<uint64_t>((size_t)n * sc_in.stride);
+    uint64_t *b = dev.arena.take<uint64_t>((size_t)n * 2 * C::NP64);
+    ZK_CHECK(hipMemcpyAsync(a, sc_in.data, sc_bytes, hipMemcpyHostToDevice, st));
+    ZK_CHECK(hipMemcpyAsync(b, points, pt_bytes, hipMemcpyHostToDevice, st));
+    sc.data = a;
+    pts_ref = b;
+  }
+  uint32_t *pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
+  uint32_t *part = dev.arena.take<uint32_t>((size_t)nbits * G * XW);
+  uint64_t *exp = dev.arena.take<uint64_t>((size_t)nbits * 4 * C::NP64);
+  hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, pts_ref, n, pts_int);
+  ZK_CHECK(hipGetLastError());
+  prof.mark("points");
+  timer_begin(dev, 0, st);
+  hipLaunchKernelGGL(k_bitacc<C>, dim3((unsigned)G), dim3(256), 0, st, sc.data, n, sc.stride, sc.loff, sc.nread,
+                     sc.mont ? 1 : 0, nbits, K, pts_int, part);
+  ZK_CHECK(hipGetLastError());
+  timer_end(dev, 0, st);
+  prof.mark("bitacc");
+  hipLaunchKernelGGL(k_bitsum<C>, dim3((unsigned)nbits), dim3(256), 0, st, part, G, exp);
+  ZK_CHECK(hipGetLastError());
+  prof.mark("bitsum");
+  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(exp_bytes + 64));
+  ZK_CHECK(hipMemcpyAsync(h, exp, exp_bytes, hipMemcpyDeviceToHost, st));
+  stream_wait(dev, st);
+  prof.mark("export");
+  timer_collect(dev);
+  const auto t0 = std::chrono::steady_clock::now();
+  constexpr int BW = 8;  // host Horner windows over the bits
+  finish_host<C>(BW, (nbits + BW - 1) / BW, h, out, nbits);
+  prof.report(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+}
+
 // Run the device pipeline for one scalar slice.  points are DEVICE pointers (or host
 // pointers when host_inputs, in which case they are staged, with the scalars).
 // Result: sum_i k_i P_i in host XYZZ (reference Montgomery form).
@@ -1731,8 +1907,15 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
     zkh::xyzz_set_inf(out);
     return;
   }
-  const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
+  const bool explicit_window = window >= 4 && window <= 24;
+  const int c = explicit_window ? window : msm_default_window(n);
   const int bits = sc_in.mont ? HostOf<C>::Fr::BITS : 64 * sc_in.nread;
+  // small inputs with the default window: bit jobs, no buckets (an explicit window -- the
+  // reference's _variable entry -- always runs the bucket method it names)
+  if (!explicit_window && n <= msm_bits_max()) {
+    msm_run_bits<C>(dev, n, sc_in, points, host_inputs, bits, out);
+    return;
+  }
   // Signed digits need floor(bits/c) + 1 windows: the top window then holds at most c-1
   // bits plus the carry, i.e. a digit <= 2^(c-1) = B, so no carry leaves it.
   const int W = bits / c + 1;
@@ -1875,8 +2058,14 @@ template <class C>
 size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int window, int groups) {
   using F = typename C::Fp;
   if (n <= 0) return 0;
-  const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
   const int nread = nl < 4 ? nl : 4;
+  if (!(window >= 4 && window <= 24) && n <= msm_bits_max()) {  // the bit-job path (msm_run_bits)
+    const int nbits = mont ? HostOf<C>::Fr::BITS : 64 * nread;
+    const size_t io = host_inputs ? (size_t)n * nl * 8 + (size_t)n * 2 * C::NP64 * 8 : 0;
+    return io + (size_t)n * aff_words<F>() * 4 + (size_t)nbits * msm_bits_groups(n) * xyzz_words<F>() * 4 +
+           (size_t)nbits * 4 * C::NP64 * 8 + 5 * 256;
+  }
+  const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
   const int W = (mont ? HostOf<C>::Fr::BITS : 64 * nread) / c + 1;
   const int g = groups < 1 ? 1 : (groups > W ? W : groups);
   const int Wg = (W + g - 1) / g;

@@ -60,7 +60,7 @@ EXTENSION_SYMBOLS = [
     "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
     "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
     "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_ntt_set_max_radix", "zkg_ntt_set_table_max",
-    "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
+    "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_g1_fft_last_glv", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
     "zkg_release", "zkg_comm_unique_id", "zkg_comm_init", "zkg_comm_destroy", "zkg_comm_rank", "zkg_comm_world",
     "zkg_comm_allgather", "zkg_comm_barrier", "zkg_comm_max_f64", "zkg_g1_comm_sum_partials",
     "zkg_g1_msm_device_sharded", "zkg_set_error_mode", "zkg_last_error",
@@ -584,6 +584,11 @@ def arena_set_limit(nbytes):
 
 def msm_last_groups():
     return load().zkg_msm_last_groups()
+
+
+def g1_fft_last_glv():
+    """1 when the most recent group FFT ran the GLV stages (all inputs in the order-r subgroup)"""
+    return load().zkg_g1_fft_last_glv()
 
 
 def msm_workspace_bytes(curve, n, nlimbs=4, mont=True, host_inputs=True, window=0, groups=1):

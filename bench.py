@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--ntt-steps", type=int, default=5)
     ap.add_argument("--no-ntt", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) rates")
+    ap.add_argument("--no-extras", action="store_true", help="skip the small-MSM sizes and the group FFT")
     ap.add_argument("--no-config4", action="store_true", help="skip the secondary BN128 2^24 (config 4) MSM line")
     ap.add_argument("--no-config5", action="store_true", help="skip the 2^26 (config 5) strong-scaling line")
     ap.add_argument("--config5-steps", type=int, default=3)
@@ -309,11 +310,93 @@ def main():
         result["config4"] = bench_config4(zk)
     if rank == 0 and world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(zk, curve, scalars, points, ms_per_step, result.get("ntt"), args, aff)
+    if rank == 0 and world == 1 and not args.no_extras:
+        result["msm_sizes"] = bench_msm_sizes(zk)
+        result["group_fft"] = bench_group_fft(zk)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(zk, curve, seed, args.cpu_msm_log, args.cpu_ntt_log)
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.close()
+
+
+def _median_ms(fn, reps):
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    ts.sort()
+    return ts[len(ts) // 2] * 1e3
+
+
+def bench_msm_sizes(zk, reps=20):
+    """Small device-resident MSMs (KZG-commit sizes, examples/KZG.hs:81,88): BLS12-381 at 2^10 /
+    2^12 / 2^16 (median of `reps` calls, each a complete MSM incl. the host finish), and the
+    reference's own outputs for its golden random_n1000 / random_n4096 cases (tests/golden) as the
+    parity check of the small-input (bit-job) path."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_io import msm_cases
+    curve = "bls12_381"
+    out = {"curve": curve, "reps": reps, "timing": "device-resident inputs, median wall time per call"}
+    gold = {name: (sc, pts, aff) for name, sc, pts, mont, aff, _ in msm_cases(curve) if name in
+            ("random_n1000", "random_n4096")}
+    for name, (sc, pts, aff) in gold.items():
+        n = sc.shape[0]
+        ds, dp = zk.DeviceBuffer(sc), zk.DeviceBuffer(pts)
+        got = zk.msm_device(curve, n, ds, dp)
+        ms = _median_ms(lambda: zk.msm_device(curve, n, ds, dp), reps)
+        ds.free()
+        dp.free()
+        aff_got = zk.msm_affine(curve, sc, pts)
+        dev_aff = zk.batch_to_affine(curve, got.reshape(1, -1))[0]
+        out[f"golden_{name}"] = {"n": n, "ms": ms, "parity_vs_reference": bool(np.array_equal(dev_aff, aff)),
+                                 "host_buffer_entry_parity": bool(np.array_equal(aff_got, aff))}
+    for lg in (10, 12, 16):
+        n = 1 << lg
+        sc, pts = zk.gen_fr(curve, 0x5A4B0002, n), zk.gen_points(curve, 0x5A4B0002, n)
+        ds, dp = zk.DeviceBuffer(sc), zk.DeviceBuffer(pts)
+        zk.msm_device(curve, n, ds, dp)
+        out[f"2^{lg}_ms"] = _median_ms(lambda: zk.msm_device(curve, n, ds, dp), reps)
+        ds.free()
+        dp.free()
+    out["bits_path_max_n"] = 4096
+    return out
+
+
+def bench_group_fft(zk, m=16, reps=3):
+    """The group (curve) FFT, <C>_G1_proj_fft_forward / _inverse (bls12_381_G1_proj.c:679-790), on
+    2^m subgroup points, device-resident: ms per transform, whether the GLV stages ran, and the
+    round trip inverse(forward(P)) == P (exact, normalised projective)."""
+    import ctypes
+    import numpy as np
+    lib = zk.load()
+    lib.zkg_g1_fft_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.c_void_p, ctypes.c_void_p]
+    out = {"log_n": m, "reps": reps}
+    for curve in ("bls12_381", "bn128"):
+        n = 1 << m
+        pts = zk.batch_from_affine(curve, zk.gen_points(curve, 0x5A4B0007, n))
+        sg = zk.get_fft_subgroup(curve, m)
+        g = sg.gen_array()
+        d_in, d_out = zk.DeviceBuffer(pts), zk.DeviceBuffer.empty(pts.nbytes)
+        r = {}
+        for name, inv in (("forward", 0), ("inverse", 1)):
+            call = lambda: lib.zkg_g1_fft_device(zk.CURVE_ID[curve], inv, m, zk._p(g), d_in.ptr, d_out.ptr)  # noqa
+            call()
+            lib.zkg_device_synchronize()
+
+            def once():
+                call()
+                lib.zkg_device_synchronize()
+            r[f"{name}_ms"] = _median_ms(once, reps)
+            r[f"{name}_glv"] = bool(zk.g1_fft_last_glv())
+        d_in.free()
+        d_out.free()
+        r["round_trip_exact"] = bool(np.array_equal(zk.inverse_fft(sg, zk.forward_fft(sg, pts)), pts))
+        out[curve] = r
+    return out
 
 
 def bench_config5(zk, args, dist):

@@ -26,7 +26,7 @@ shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 O=gpurun_out/$TAG
-BENCH_SHORT="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-config4 --no-config5 --ntt-steps 3"
+BENCH_SHORT="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e --no-config4 --no-config5 --ntt-steps 3 --no-extras"
 for step in "$@"; do
   echo "[$(date +%T)] step $step"
   case $step in

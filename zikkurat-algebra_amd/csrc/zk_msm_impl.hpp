@@ -1433,7 +1433,6 @@ static size_t group_bytes(const MsmShape &s) {
   add(ns1 * (xw + 4) * 2);                // stitch ping-pong
   add(nb * xw);                           // buckets
   add((size_t)s.W * s.NY * xw);           // Y
-  add((size_t)s.W * s.J * 4 * C::NP64 * 8);  // export
   add(cub > cub2 ? cub : cub2);
   if (s.NS > 1) add(cub > cub2 ? cub : cub2);  // the sort stream's own scan scratch
   return bytes + (1 << 20);
@@ -1511,7 +1510,6 @@ struct GroupPass {
   uint32_t *list, *dig, *tmpv, *cnt, *coff, *offsets, *ikeys0, *ivals0, *ckeys, *cidx, *flags, *pos, *ccount;
   uint16_t *tmpf;
   uint32_t *okA, *ovA, *okB, *ovB, *buckets, *Y;
-  uint64_t *exp;
   void *cubtmp;
   uint8_t *filled = nullptr;  // split pipelines: bucket b holds a sum from an earlier split
   // host inputs: the sorts run on their own stream (sst, with their own scan scratch) beside the
@@ -1558,7 +1556,6 @@ struct GroupPass {
     ovB = dev.arena.take<uint32_t>(ns1 * xw);
     buckets = dev.arena.take<uint32_t>(nb * xw);
     Y = dev.arena.take<uint32_t>((size_t)s.W * s.NY * xw);
-    exp = dev.arena.take<uint64_t>((size_t)s.W * s.J * 4 * C::NP64);
     size_t cub2 = 0;
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, cnt, coff, (int)(s.nmat() + 1), st));
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
@@ -1717,11 +1714,11 @@ struct GroupPass {
     }
     ZK_CHECK(hipGetLastError());
     mark("ysum");
-    hipLaunchKernelGGL(k_jobsum_blk<C>, dim3((unsigned)(s.W * c)), dim3(256), 0, st, Y, c, s.l0, exp);
+    // the job sums land straight in the pinned host buffer (mapped at the same address on the
+    // device): no copy, and no copy-engine start-up after the last kernel
+    hipLaunchKernelGGL(k_jobsum_blk<C>, dim3((unsigned)(s.W * c)), dim3(256), 0, st, Y, c, s.l0, h);
     ZK_CHECK(hipGetLastError());
     mark("jobsum");
-    const int ngrp = s.W * s.J;
-    ZK_CHECK(hipMemcpyAsync(h, exp, (size_t)ngrp * 4 * C::NP64 * 8, hipMemcpyDeviceToHost, st));
   }
 
   // Everything is enqueued without a host round trip.  The stitch levels are deterministic: a
@@ -1774,6 +1771,10 @@ static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typena
   std::vector<zkh::Jac<HF>> V(W);
   std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[W]);
   for (int w = 0; w < W; w++) ready[w].store(0, std::memory_order_relaxed);
+  // windows are claimed top first from one counter, by the pool's workers and by the calling
+  // thread whenever the chain reaches a window nobody has finished: the chain never waits for a
+  // worker's wake-up (~50 us), and a window is never computed twice
+  std::atomic<int> next_win{0};
   auto window = [&](int i) {
     const int w = W - 1 - i;
     std::vector<zkh::Xyzz<HF>> Z(E);
@@ -1801,14 +1802,22 @@ static void finish_host(int c, int W, const uint64_t *exported, zkh::Xyzz<typena
   };
   zkh::Jac<HF> acc;
   zkh::jac_set_inf(acc);
+  auto claim = [&]() -> bool {  // computes the next unclaimed window; false when none is left
+    const int i = next_win.fetch_add(1);
+    if (i >= W) return false;
+    window(i);
+    return true;
+  };
   auto chain = [&] {
     for (int w = W - 1; w >= 0; w--) {
       for (int k = 0; k < c; k++) zkh::jac_dbl(acc, acc);
-      while (!ready[w].load(std::memory_order_acquire)) std::this_thread::yield();
+      while (!ready[w].load(std::memory_order_acquire))
+        if (!claim()) std::this_thread::yield();
       zkh::jac_add(acc, acc, V[w]);
     }
   };
-  host_parallel_for_main(W, window, chain);
+  const int nthreads = W < 8 ? W : 8;
+  host_parallel_for_main(nthreads, [&](int) { while (claim()) {} }, chain);
   zkh::jac_to_xyzz(out, acc);
 }
 
@@ -1851,7 +1860,7 @@ static void msm_run_bits(Device &dev, int n, const ScalarSlice &sc_in, const uin
   const size_t int_bytes = (size_t)n * aff_words<F>() * 4;
   const size_t part_bytes = (size_t)nbits * G * XW * 4;
   const size_t exp_bytes = (size_t)nbits * 4 * C::NP64 * 8;
-  const size_t need = sc_bytes + pt_bytes + int_bytes + part_bytes + exp_bytes + 5 * 256;
+  const size_t need = sc_bytes + pt_bytes + int_bytes + part_bytes + 4 * 256;
   if (!dev.arena.try_reserve(need)) {
     ZK_CHECK(hipStreamSynchronize(st));
     ntt_release(dev);
@@ -1872,7 +1881,7 @@ static void msm_run_bits(Device &dev, int n, const ScalarSlice &sc_in, const uin
   }
   uint32_t *pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
   uint32_t *part = dev.arena.take<uint32_t>((size_t)nbits * G * XW);
-  uint64_t *exp = dev.arena.take<uint64_t>((size_t)nbits * 4 * C::NP64);
+  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(exp_bytes + 64));  // k_bitsum writes here
   hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, pts_ref, n, pts_int);
   ZK_CHECK(hipGetLastError());
   prof.mark("points");
@@ -1882,11 +1891,9 @@ static void msm_run_bits(Device &dev, int n, const ScalarSlice &sc_in, const uin
   ZK_CHECK(hipGetLastError());
   timer_end(dev, 0, st);
   prof.mark("bitacc");
-  hipLaunchKernelGGL(k_bitsum<C>, dim3((unsigned)nbits), dim3(256), 0, st, part, G, exp);
+  hipLaunchKernelGGL(k_bitsum<C>, dim3((unsigned)nbits), dim3(256), 0, st, part, G, h);
   ZK_CHECK(hipGetLastError());
   prof.mark("bitsum");
-  uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(exp_bytes + 64));
-  ZK_CHECK(hipMemcpyAsync(h, exp, exp_bytes, hipMemcpyDeviceToHost, st));
   stream_wait(dev, st);
   prof.mark("export");
   timer_collect(dev);
@@ -2062,8 +2069,7 @@ size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int windo
   if (!(window >= 4 && window <= 24) && n <= msm_bits_max()) {  // the bit-job path (msm_run_bits)
     const int nbits = mont ? HostOf<C>::Fr::BITS : 64 * nread;
     const size_t io = host_inputs ? (size_t)n * nl * 8 + (size_t)n * 2 * C::NP64 * 8 : 0;
-    return io + (size_t)n * aff_words<F>() * 4 + (size_t)nbits * msm_bits_groups(n) * xyzz_words<F>() * 4 +
-           (size_t)nbits * 4 * C::NP64 * 8 + 5 * 256;
+    return io + (size_t)n * aff_words<F>() * 4 + (size_t)nbits * msm_bits_groups(n) * xyzz_words<F>() * 4 + 4 * 256;
   }
   const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
   const int W = (mont ? HostOf<C>::Fr::BITS : 64 * nread) / c + 1;

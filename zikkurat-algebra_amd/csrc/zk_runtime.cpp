@@ -79,8 +79,11 @@ Arena::~Arena() {
 void *Device::host_staging(size_t bytes) {
   if (bytes > pinned_cap) {
     if (pinned) ZK_CHECK(hipHostFree(pinned));
-    ZK_CHECK(hipHostMalloc(&pinned, bytes, hipHostMallocDefault));
+    ZK_CHECK(hipHostMalloc(&pinned, bytes, hipHostMallocMapped | hipHostMallocCoherent));
     pinned_cap = bytes;
+    void *dp = nullptr;
+    ZK_CHECK(hipHostGetDevicePointer(&dp, pinned, 0));
+    ZK_REQUIRE(dp == pinned, "pinned staging: the device address differs from the host address");
   }
   return pinned;
 }
@@ -204,15 +207,17 @@ void stream_wait(Device &dev, hipStream_t st) {
   if (!dev.sync_ev) ZK_CHECK(hipEventCreateWithFlags(&dev.sync_ev, hipEventDisableTiming));
   ZK_CHECK(hipEventRecord(dev.sync_ev, st));
   // spin for the first 0.2 ms (the wake-up latency of a blocking wait is ~0.1 ms, which the
-  // short calls would pay in full), then yield, and beyond 2 ms sleep 20 us between polls so
-  // long calls (host-buffer copies, large transforms) do not pin a host core
+  // short calls would pay in full), then yield, and beyond 20 ms sleep 20 us between polls so
+  // long calls (config-5 MSMs, 2^26 transforms) do not pin a host core.  (Round 3 slept from
+  // 2 ms on: a 20 us sleep returns after ~50-100 us on the host, which every 2-20 ms call -- the
+  // 2^20 MSM, the 2^24 NTT -- paid at its end: BLS12-381 2^20 export phase 0.07 vs 0.02 ms at 2^16.)
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t e = hipEventQuery(dev.sync_ev);
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) ZK_CHECK(e);
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    if (us > 2000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if (us > 20000) std::this_thread::sleep_for(std::chrono::microseconds(20));
     else if (us > 200) std::this_thread::yield();
   }
 }

@@ -139,7 +139,8 @@ struct Device {
   hipStream_t stream = nullptr;
   Arena arena;
   std::mutex mu;
-  // pinned host staging for small D2H results
+  // pinned host staging for small D2H results; fine-grained and mapped at the same address on
+  // the device, so kernels write their exports into it directly (the MSM's job sums)
   void *pinned = nullptr;
   size_t pinned_cap = 0;
   void *host_staging(size_t bytes);

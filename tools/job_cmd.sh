@@ -1,10 +1,6 @@
-# r04s: split weights x copy mode (host-buffer MSM 2^20)
+# r04t: GLV FFT with the pair-shared table and the sparse-z membership test
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-for rep in 1 2; do
-  for m in 0 2; do
-    for w in "2,3,4,4,3" "2,4,5,5" "2,3,4,5,2" "1,2,4,5,4" "3,4,4,3,2" "2,2,3,3,3,3"; do
-      echo "== mode $m split $w"; ZK_COPY_MODE=$m ZK_MSM_SPLIT_W=$w timeout -k 10 120 python -u tools/e2e_probe.py bls12_381 20 15 2>&1 | grep -v amdgpu.ids || exit 1
-    done
-  done
-done
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_g1ext.py -m gpu 2>&1 | tail -3 || exit 1
+timeout -k 10 300 python -u tools/fft_time.py 16 3 check 2>&1 | grep -v amdgpu.ids || exit 1
+timeout -k 10 300 python -u tools/fft_time.py 16 3 2>&1 | grep -v amdgpu.ids || exit 1

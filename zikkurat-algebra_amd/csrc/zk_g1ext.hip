@@ -582,25 +582,30 @@ __device__ __forceinline__ uint32_t win5_3(const uint64_t *K, int i) {
   if (o > 59 && w < 2) v |= K[w + 1] << (64 - o);
   return (uint32_t)v & 31u;
 }
-// r = k p for k < 2^130 (3 words), p finite: 16-entry table, 27 signed 5-bit windows
-// (K = k + 16 sum_{i<27} 32^i < 2^135)
+// The pair's shared table: d P for d = 1..16 built by both lanes (lane 0 the odd d, lane 1 the
+// even d, stepping by 2P: one doubling and 7 additions each instead of 15 additions per lane),
+// stored at the pair's slot; lane 1 uses phi(d P) = (beta X, Y, Z) at lookup (one product per
+// window).  The halves are read back by the other lane of the wavefront: the stores are
+// released and the CU's L1 invalidated (agent-scope fences) before the lookups.
+// r = k (phi^q P) for k < 2^130, signs applied at lookup (neg: the half's scalar is negative)
 template <class F>
-__device__ __forceinline__ void jac_scl130(Jac<F> &acc, const Jac<F> &p, const uint64_t *k, uint32_t *__restrict__ tab) {
+__device__ __forceinline__ void jac_scl130_pair(Jac<F> &acc, const Jac<F> &p, const uint64_t *k, bool neg,
+                                                const Fe<F> &mulx, uint32_t *__restrict__ tab) {
+  const int q = (int)(threadIdx.x & 1);
   {
-    Jac<F> a;
-    JacC<F> pc, c;
-    jac_cache(pc, p);
-    jacc_store(tab, pc);
-    a = p;
-    jac_dbl(a);
-    jac_cache(c, a);
-    jacc_store(tab + 1 * 5 * F::SN, c);
-    for (int d = 3; d <= SCL_TAB; d++) {
-      jac_add_cached(a, pc);
+    Jac<F> two = p, a;
+    jac_dbl(two);
+    JacC<F> c2, c;
+    jac_cache(c2, two);
+    a = q ? two : p;
+    for (int i = 0; i < SCL_TAB / 2; i++) {
+      if (i) jac_add_cached(a, c2);
       jac_cache(c, a);
-      jacc_store(tab + (size_t)(d - 1) * 5 * F::SN, c);
+      jacc_store(tab + (size_t)(q + 2 * i) * 5 * F::SN, c);
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   uint64_t K[3];
   {
     const uint64_t H[3] = {0x0842108421084210ull, 0x1084210842108421ull, 0x0000000000000042ull};
@@ -623,7 +628,10 @@ __device__ __forceinline__ void jac_scl130(Jac<F> &acc, const Jac<F> &p, const u
     if (d) {
       JacC<F> e;
       jacc_load(e, tab + (size_t)((d < 0 ? -d : d) - 1) * 5 * F::SN);
-      if (d < 0) {
+      Fe<F> x;
+      fe_mul(x, e.X, mulx);  // lane 1: phi
+      e.X = x;
+      if ((d < 0) != neg) {
         Fe<F> ny;
         fe_neg(ny, e.Y);
         e.Y = ny;
@@ -646,17 +654,11 @@ __device__ __forceinline__ void glv_scl_pair(Xyzz<F> &t, const Xyzz<F> &v, const
   } else {
     Jac<F> p;
     xyzz_to_jac(p, v);
-    if (q) {
-      Fe<F> bx;
-      fe_mul(bx, p.X, beta);
-      p.X = bx;
-    }
-    if ((dk[6] >> q) & 1) {
-      Fe<F> ny;
-      fe_neg(ny, p.Y);
-      p.Y = ny;
-    }
-    jac_scl130(r, p, dk + 3 * q, tab);
+    Fe<F> mulx;
+    if (q) mulx = beta;
+    else fe_one(mulx);
+    // the pair's table lives in lane 0's scratch slot
+    jac_scl130_pair(r, p, dk + 3 * q, ((dk[6] >> q) & 1) != 0, mulx, tab - (size_t)q * scl_tab_words<F>());
   }
   Jac<F> o;
   fe_pair_swap(o.X, r.X);
@@ -754,6 +756,22 @@ __global__ void __launch_bounds__(256) k_fft_scale_glv(int n, const uint32_t *__
   }
 }
 
+// r = [|z|] p for BLS12-381's z = -0xd201000000010000 (bits 63, 62, 60, 57, 48, 16): 63 doublings
+// and 5 additions, the membership test's chain (k_subgroup_check)
+template <class F>
+__device__ __forceinline__ void jac_mul_absz(Jac<F> &r, const Jac<F> &p) {
+  JacC<F> pc;
+  jac_cache(pc, p);
+  r = p;
+  for (int b = 62; b >= 0; b--) {
+    jac_dbl(r);
+    if (b == 62 || b == 60 || b == 57 || b == 48 || b == 16) {
+      if (jac_is_inf(p)) continue;
+      jac_add_cached(r, pc);
+    }
+  }
+}
+
 // subgroup membership (curves with a cofactor): phi(P) == [lambda] P for every point (lambda
 // 128 bits on BLS12-381; tools/gen_glv.py checks the test on subgroup and non-subgroup points).
 // bad[block] = 1 when some point of the block fails.
@@ -765,7 +783,6 @@ __global__ void __launch_bounds__(256) k_subgroup_check(int n, const uint32_t *_
   Fe<F> beta, t0;
   fe_load_ref(t0, beta_ref.w);
   fe_to_int(beta, t0);
-  uint32_t *tab = scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>();
   int fail = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += (size_t)lanes) {
     Xyzz<F> v;
@@ -773,7 +790,16 @@ __global__ void __launch_bounds__(256) k_subgroup_check(int n, const uint32_t *_
     if (xyzz_is_inf(v)) continue;
     Jac<F> p, r;
     xyzz_to_jac(p, v);
-    jac_scl130(r, p, gp.lambda, tab);
+    {  // [lambda] P = [|z|]([|z|] P) - P (lambda = z^2 - 1; |z| = 0xd201000000010000 has 6 bits set)
+      Jac<F> zp;
+      jac_mul_absz(zp, p);
+      jac_mul_absz(r, zp);
+      Jac<F> np = p;
+      fe_neg(np.Y, p.Y);
+      JacC<F> nc;
+      jac_cache(nc, np);
+      jac_add_cached(r, nc);
+    }
     if (jac_is_inf(r)) {
       fail = 1;
       continue;

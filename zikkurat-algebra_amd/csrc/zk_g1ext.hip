@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(256) k_fft_fwd_stage_glv(int m, int s, const u
   }
 }
 
-// inverse DIF stage on lane pairs, factor 1/2 per level deferred (k_fft_scale_glv applies N^-1
+// inverse DIF stage on lane pairs, factor 1/2 per level deferred (k_fft_inv_first_glv applies N^-1
 // once): lane 0 writes u + v, lane 1 (u - v) w^-j
 template <class C>
 __global__ void __launch_bounds__(256) k_fft_inv_stage_glv(int m, int s, const uint32_t *__restrict__ A,
@@ -737,22 +737,37 @@ __global__ void __launch_bounds__(256) k_fft_inv_stage_glv(int m, int s, const u
   }
 }
 
-// every point times one decomposed scalar dk (the inverse's N^-1), lane pairs
+// the inverse's FIRST stage (s = m) with the deferred N^-1 applied to both outputs: four lanes
+// per butterfly, pair 0 -> (u + v) N^-1 (dkn), pair 1 -> (u - v) w^-j N^-1 (twn[j], the twiddle
+// with N^-1 folded in) -- one doubled stage instead of a stage plus a scaling pass over N points
 template <class C>
-__global__ void __launch_bounds__(256) k_fft_scale_glv(int n, const uint32_t *__restrict__ A, uint32_t *__restrict__ B,
-                                                       const uint64_t *__restrict__ dk, W6 beta_ref,
-                                                       uint32_t *__restrict__ scratch, int lanes) {
+__global__ void __launch_bounds__(256) k_fft_inv_first_glv(int m, const uint32_t *__restrict__ A,
+                                                           uint32_t *__restrict__ B, const uint64_t *__restrict__ twn,
+                                                           const uint64_t *__restrict__ dkn, W6 beta_ref,
+                                                           uint32_t *__restrict__ scratch, int lanes) {
   using F = typename C::Fp;
+  const size_t half = (size_t)1 << (m - 1);
+  const size_t nl = (size_t)1 << (m + 1);  // 4 lanes x N / 2 butterflies
   Fe<F> beta, t0;
   fe_load_ref(t0, beta_ref.w);
   fe_to_int(beta, t0);
   uint32_t *tab = scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>();
-  for (size_t L = (size_t)blockIdx.x * blockDim.x + threadIdx.x; L < 2 * (size_t)n; L += (size_t)lanes) {
-    const size_t i = L >> 1;
-    Xyzz<F> v, t;
-    xyzz_load(v, A + i * xw<F>());
-    glv_scl_pair(t, v, dk, beta, tab);
-    if ((L & 1) == 0) xyzz_store(B + i * xw<F>(), t);
+  for (size_t L = (size_t)blockIdx.x * blockDim.x + threadIdx.x; L < nl; L += (size_t)lanes) {
+    const size_t j = L >> 2;  // s = m: one block, k0 = j
+    const int pr = (int)((L >> 1) & 1);
+    Xyzz<F> u, v, d, t;
+    xyzz_load(u, A + j * xw<F>());
+    xyzz_load(v, A + (j + half) * xw<F>());
+    d = u;
+    if (pr) {
+      Xyzz<F> nv;
+      xyzz_neg(nv, v);
+      xyzz_add(d, nv);
+    } else {
+      xyzz_add(d, v);
+    }
+    glv_scl_pair(t, d, pr ? twn + j * 8 : dkn, beta, tab);
+    if ((L & 1) == 0) xyzz_store(B + (j + (pr ? half : 0)) * xw<F>(), t);
   }
 }
 
@@ -1002,7 +1017,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   const size_t tlanes = std::max(lanes, glanes);
   const size_t nbad = div_up(N, 256);
   dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 2 * N * xw<F>() * 4 + tlanes * scl_tab_words<F>() * 4 +
-                    tw_cnt * 32 + tw_cnt * 64 + 64 + nbad * 4 + N * NP * 8 + (1 << 20));
+                    tw_cnt * 32 + 2 * tw_cnt * 64 + 64 + nbad * 4 + N * NP * 8 + (1 << 20));
   dev.arena.reset();
   const uint64_t *ds = src;
   uint64_t *dt = tgt;
@@ -1016,7 +1031,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   uint32_t *B = dev.arena.take<uint32_t>(N * xw<F>());
   uint32_t *scratch = dev.arena.take<uint32_t>(tlanes * scl_tab_words<F>());
   uint64_t *tw = dev.arena.take<uint64_t>(tw_cnt * 4);
-  uint64_t *twg = dev.arena.take<uint64_t>(tw_cnt * 8 + 8);
+  uint64_t *twg = dev.arena.take<uint64_t>(2 * tw_cnt * 8 + 8);  // w^e, then (w^-1)^e N^-1, then N^-1
   uint32_t *bad = dev.arena.take<uint32_t>(nbad);
   uint64_t *nscratch = dev.arena.take<uint64_t>(N * NP);
 
@@ -1044,7 +1059,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   g1_fft_last_glv().store(glv ? 1 : 0);
   if (glv) {
     // twiddles (decomposed): forward w^e; inverse (w^-1)^e with the 1/2 per level deferred to one
-    // final multiplication by N^-1 (on the subgroup ((u + v) / 2 ...) over m levels = N^-1 (...))
+    // multiplication by N^-1 folded into the first stage (on the subgroup the m halvings = N^-1)
     zkh::Fe<HR> g, one, ninv;
     memcpy(g.v, gen, sizeof g.v);
     zkh::set_one(one);
@@ -1055,7 +1070,24 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
     ZK_CHECK(hipGetLastError());
     const unsigned grid = (unsigned)(glanes / 256);
     uint32_t *in = A, *out = B;
-    for (int k = 0; k < m; k++) {
+    int k0 = 0;
+    if (inverse) {  // first stage with N^-1 folded in: twn = (w^-1)^j N^-1, dkn = N^-1 (decomposed)
+      zkh::Fe<HR> nn = one;
+      for (int k = 0; k < m; k++) zkh::add(nn, nn, nn);
+      zkh::inv(ninv, nn);
+      for (int j = 0; j < 4; j++) wn.w[j] = ninv.v[j];
+      uint64_t *twn = twg + tw_cnt * 8, *dkn = twg + 2 * tw_cnt * 8;
+      hipLaunchKernelGGL(k_fft_tw_glv<Fr>, dim3(div_up(tw_cnt, 256)), dim3(256), 0, st, (int)tw_cnt, wb, wn, gp, twn);
+      ZK_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(k_fft_tw_glv<Fr>, dim3(1), dim3(256), 0, st, 1, wb, wn, gp, dkn);
+      ZK_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(k_fft_inv_first_glv<C>, dim3(grid), dim3(256), 0, st, m, in, out, twn, dkn, beta, scratch,
+                         (int)glanes);
+      ZK_CHECK(hipGetLastError());
+      std::swap(in, out);
+      k0 = 1;
+    }
+    for (int k = k0; k < m; k++) {
       const int s = inverse ? m - k : k + 1;
       if (inverse)
         hipLaunchKernelGGL(k_fft_inv_stage_glv<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, twg, beta, scratch,
@@ -1063,19 +1095,6 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
       else
         hipLaunchKernelGGL(k_fft_fwd_stage_glv<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, twg, beta, scratch,
                            (int)glanes);
-      ZK_CHECK(hipGetLastError());
-      std::swap(in, out);
-    }
-    if (inverse) {  // N^-1, decomposed like a twiddle (entry 0 of a one-entry table)
-      zkh::Fe<HR> nn = one;
-      for (int k = 0; k < m; k++) zkh::add(nn, nn, nn);
-      zkh::inv(ninv, nn);
-      for (int j = 0; j < 4; j++) wn.w[j] = ninv.v[j];
-      uint64_t *dk = twg + tw_cnt * 8;
-      hipLaunchKernelGGL(k_fft_tw_glv<Fr>, dim3(1), dim3(256), 0, st, 1, wb, wn, gp, dk);
-      ZK_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(k_fft_scale_glv<C>, dim3(grid), dim3(256), 0, st, (int)N, in, out, dk, beta, scratch,
-                         (int)glanes);
       ZK_CHECK(hipGetLastError());
       std::swap(in, out);
     }

@@ -22,6 +22,23 @@ def ntt_cases(curve):
         yield m, z[f"m{m}__gen"], z[f"m{m}__input"], z[f"m{m}__forward"], z[f"m{m}__inverse"]
 
 
+def skew_scalars(gen_fr, curve, seed, n, kind):
+    """skewed scalar vectors of the large-sort tests (tests/test_gpu_msm.py, golden outputs from
+    tools/make_golden.py): "mix3" = three Fr values (Montgomery) drawn uniformly, 5 % zeros;
+    "binary" = Montgomery 0 / 1 (each with probability 1/2)"""
+    rng = np.random.default_rng(seed)
+    if kind == "mix3":
+        vals = gen_fr(curve, seed + 1, 3)
+        sc = vals[rng.integers(0, 3, n)].copy()
+        sc[rng.random(n) < 0.05] = 0
+        return sc
+    m1 = mont_one(curve)
+    one = np.array([(m1 >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)], dtype=np.uint64)
+    sc = np.zeros((n, 4), dtype=np.uint64)
+    sc[rng.random(n) < 0.5] = one
+    return sc
+
+
 def baseline_configs():
     p = os.path.join(GOLD, "baseline_configs.json")
     return json.load(open(p)) if os.path.exists(p) else {}

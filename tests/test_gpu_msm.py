@@ -75,6 +75,31 @@ def test_skewed_large_vs_reference(gpu, reference, curve):
     assert np.array_equal(gpu.msm_affine(curve, sc, pts), reference.msm(curve, sc, pts, mont=True))
 
 
+@pytest.mark.parametrize("key", ["skew_mix3_bls12_381_msm_2^22", "skew_binary_bn128_msm_2^22"])
+def test_skewed_2_22_sub_bin_sort_vs_reference(gpu, key):
+    """2^22 pairs with skewed scalars (three values + zeros, or 0 / 1: a few buckets hold ~n/3 or
+    n/2 entries), against the reference's own output (tools/make_golden.py, shards added by the
+    reference's proj_add): through the host-buffer entry (split pipelines at c = 16, each split
+    sorted in its own list region) and device-resident at c = 20, where the coarse bins (16K
+    entries, 2048 fine buckets each) outgrow level 2's LDS staging and the sort runs the sub-bin
+    level (k_split)."""
+    from golden_io import skew_scalars
+    cfg = baseline_configs().get(key)
+    if cfg is None:
+        pytest.skip(f"{key} missing")
+    curve, n = cfg["curve"], 1 << cfg["log_n"]
+    sc = skew_scalars(gpu.gen_fr, curve, cfg["seed"], n, cfg["kind"])
+    pts = gpu.gen_points(curve, cfg["seed"], n)
+    assert [int(x) for x in gpu.msm_affine(curve, sc, pts)] == cfg["affine"]
+    ds, dp = gpu.DeviceBuffer(sc), gpu.DeviceBuffer(pts)
+    try:
+        proj = gpu.msm_device(curve, n, ds, dp, window=20)
+    finally:
+        ds.free()
+        dp.free()
+    assert [int(x) for x in gpu.batch_to_affine(curve, proj.reshape(1, -1))[0]] == cfg["affine"]
+
+
 @pytest.mark.parametrize("curve", CURVES)
 @pytest.mark.parametrize("window,logn", [(0, 18), (0, 20), (17, 18)])
 def test_binary_scalars_vs_oracle(gpu, oracle, curve, window, logn):

@@ -168,6 +168,31 @@ def large_msm(curve, logn, seed, shards):
             "reference_entry": "MSM_mont_coeff_proj_out" if mont else "MSM_std_coeff_proj_out (to_std scalars)"}
 
 
+def _shard_skew(args):
+    curve, seed, kind, n, lo, hi = args
+    sc = golden_io.skew_scalars(zk.gen_fr, curve, seed, n, kind)[lo:hi].copy()
+    pts = zk.gen_points(curve, seed, hi - lo, start=lo)
+    ref = Reference()
+    t = time.time()
+    p = ref.msm(curve, sc, pts, mont=True, out="proj")
+    return p, time.time() - t
+
+
+def large_skew_msm(curve, logn, seed, kind, shards=8):
+    n = 1 << logn
+    step = n // shards
+    with mp.Pool(min(shards, 8)) as pool:
+        parts = pool.map(_shard_skew, [(curve, seed, kind, n, k * step, (k + 1) * step) for k in range(shards)])
+    ref = Reference()
+    acc = parts[0][0]
+    for p, _ in parts[1:]:
+        acc = ref.proj_add(curve, acc, p)
+    aff = ref.to_affine(curve, acc)
+    return {"curve": curve, "log_n": logn, "seed": seed, "kind": kind, "affine": [int(x) for x in aff],
+            "reference_cpu_seconds_sum_over_shards": sum(t for _, t in parts), "shards": shards,
+            "reference_entry": "MSM_mont_coeff_proj_out (shards added with proj_add)"}
+
+
 # ----------------------------------------------------------------------------- adversarial NTT patterns
 
 PATTERN_SIZES = (5, 12, 14, 20)
@@ -232,6 +257,9 @@ def make_large(which):
         "config3_bls12_381_ntt_2^24": lambda: large_ntt("bls12_381", 24, 0x5A4B0003),
         "config4_bn128_msm_2^24": lambda: large_msm("bn128", 24, 0x5A4B0004, 8),
         "config5_bls12_381_msm_2^26": lambda: large_msm("bls12_381", 26, 0x5A4B0005, 8),
+        # skewed inputs at a size whose sort takes the sub-bin level (k_split)
+        "skew_mix3_bls12_381_msm_2^22": lambda: large_skew_msm("bls12_381", 22, 0x5A4B0006, "mix3"),
+        "skew_binary_bn128_msm_2^22": lambda: large_skew_msm("bn128", 22, 0x5A4B0007, "binary"),
     }
     for k, fn in jobs.items():
         if which and which not in k:

@@ -267,6 +267,82 @@ __global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig
   }
 }
 
+// Level 1.5 (large inputs, whose coarse bins outgrow level 2's LDS staging: BLS12-381 2^26 at
+// c = 20 has bins of ~2^18 entries against 8192, and scattering them straight to 2048 fine
+// buckets cost 24 ms of a 165 ms MSM, profiles/r04v_*): every coarse bin q is split by the top
+// bits of its fine index into nsub sub-bins with the level-1 machinery -- workgroup g of the bin
+// takes its share of the bin's range, per-workgroup LDS histograms go to a (bin, sub-bin,
+// workgroup) matrix, an exclusive scan of it gives every run's slot, the scatter goes through LDS
+// in chunks and leaves in runs.  Level 2 then sorts sub-bins of ~cap / 2 entries in LDS.  Sub-bin
+// q' = q nsub + sub owns fine buckets [sub F', (sub + 1) F') of bin q (F' = F / nsub), so level 2's
+// offsets[q' F' + f'] are exactly offsets[q F + f]: the layout downstream is unchanged.
+template <bool SCATTER>
+__global__ void __launch_bounds__(256) k_split(const uint32_t *__restrict__ coff, int nwg, int s2sh, int nsub,
+                                               uint32_t *__restrict__ mat, const uint32_t *__restrict__ tmpv,
+                                               const uint16_t *__restrict__ tmpf, uint32_t *__restrict__ outv,
+                                               uint16_t *__restrict__ outf) {
+  __shared__ uint32_t hist[256], lofs[256], gcur[256], scan_tmp[256];
+  __shared__ uint32_t sv[SORT_CHUNK], sk[SORT_CHUNK];
+  const uint32_t q = blockIdx.y, g = blockIdx.x, nwg2 = gridDim.x;
+  const int t = threadIdx.x;
+  const uint32_t start = coff[(size_t)q * nwg], end = coff[(size_t)(q + 1) * nwg];
+  const uint32_t len = end - start, per = (len + nwg2 - 1) / nwg2;
+  const uint32_t e0 = start + min(len, g * per), e1 = start + min(len, (g + 1) * per);
+  // mat: the (bin, sub-bin, workgroup) counts (count pass) or their exclusive scan (scatter pass);
+  // the bin's range always comes from the level-1 scan coff
+  uint32_t *cw = mat + (size_t)q * nsub * nwg2 + g;
+  const uint32_t lmask = (1u << s2sh) - 1;
+  if (!SCATTER) {
+    if (q == 0 && g == 0 && t == 0) mat[(size_t)gridDim.y * nsub * nwg2] = 0;  // the scan's total slot
+    for (int b = t; b < nsub; b += 256) hist[b] = 0;
+    __syncthreads();
+    for (uint32_t e = e0 + t; e < e1; e += 256) atomicAdd(&hist[(uint32_t)tmpf[e] >> s2sh], 1u);
+    __syncthreads();
+    for (int b = t; b < nsub; b += 256) cw[(size_t)b * nwg2] = hist[b];
+    return;
+  }
+  for (int b = t; b < nsub; b += 256) gcur[b] = cw[(size_t)b * nwg2];
+  constexpr int PER = SORT_CHUNK / 256;
+  for (uint32_t c0 = e0; c0 < e1; c0 += SORT_CHUNK) {
+    for (int b = t; b < nsub; b += 256) hist[b] = 0;
+    __syncthreads();
+    uint32_t val[PER], key[PER], rank[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      const uint32_t e = c0 + k * 256 + t;
+      key[k] = 0xffffffffu;
+      if (e < e1) {
+        key[k] = tmpf[e];
+        val[k] = tmpv[e];
+        rank[k] = atomicAdd(&hist[key[k] >> s2sh], 1u);
+      }
+    }
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t h = t < nsub ? hist[t] : 0u;
+    const uint32_t ex = block_excl_scan256(h, scan_tmp, &tot);
+    if (t < nsub) lofs[t] = ex;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+      if (key[k] != 0xffffffffu) {
+        const uint32_t p = lofs[key[k] >> s2sh] + rank[k];
+        sv[p] = val[k];
+        sk[p] = key[k];
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < tot; i += 256) {
+      const uint32_t k = sk[i], b = k >> s2sh;
+      const uint32_t slot = gcur[b] + (i - lofs[b]);
+      outv[slot] = sv[i];
+      outf[slot] = (uint16_t)(k & lmask);
+    }
+    __syncthreads();
+    if (t < nsub) gcur[t] += h;
+  }
+}
+
 // LDS counter increments with wavefront aggregation: lanes that hit the same counter are served
 // by ONE atomic (leader = the lowest such lane) for up to 4 keys with >= 4 lanes each; the rest
 // use plain per-lane atomics.  A bin whose entries share a few fine buckets -- binary 0/1 scalar
@@ -1244,6 +1320,9 @@ struct MsmShape {
   // two-level bucket sort: 2^fs fine buckets per coarse bin, nbins coarse bins per window,
   // level-1 workgroups of M entries (nwg per window)
   int fs, nbins, M, nwg;
+  // level 1.5 (k_split): 2^s2 sub-bins per coarse bin (0: none), nwg2 workgroups per bin
+  int s2 = 0, nwg2 = 1;
+  size_t nmat2() const { return (size_t)W * nbins * ((size_t)1 << s2) * nwg2; }
   // point splits: the entries are sorted by (split, window, bucket), split h holding the pairs
   // [split_lo(h), split_lo(h + 1)); each split is accumulated by its own launch (host-input calls
   // start on the first split while the later splits' points still cross PCIe)
@@ -1355,6 +1434,22 @@ static MsmShape make_shape(int n, int c, int W, int NS = 1) {
     M = (M + 255) & ~(size_t)255;
     s.M = (int)(M < 2048 ? 2048 : M);
     s.nwg = (int)(((size_t)s.nsplit_max() + s.M - 1) / s.M);
+    // sub-bins when an average coarse bin exceeds half of level 2's LDS staging AND has >= 1024
+    // fine buckets to scatter to (c >= 19: 2^25-2^26 at the default window; BLS12-381 2^26 sort
+    // 31.6 -> 15.6 ms).  With c = 16's 128 fine buckets per bin the direct scatter stays cheaper
+    // than the extra pass (2^21-2^24: +0.2 to +1.4 ms, profiles/r04x_*).  ZK_SORT_SPLIT=0 turns
+    // level 1.5 off (A/B hook, read once)
+    static const bool split_on = [] {
+      const char *e = getenv("ZK_SORT_SPLIT");
+      return !(e && e[0] == '0');
+    }();
+    const size_t per_bin = (size_t)s.nsplit_max() / s.nbins;
+    const size_t half_cap = (size_t)fine_stage_cap(s.fs) / 2;
+    while (split_on && s.fs >= 10 && s.s2 < s.fs && s.s2 < 8 && (per_bin >> s.s2) > half_cap) s.s2++;
+    if (s.s2) {
+      const size_t w2 = per_bin / 16384;  // ~16K entries per level-1.5 workgroup
+      s.nwg2 = (int)(w2 < 1 ? 1 : (w2 > 64 ? 64 : w2));
+    }
   }
   // entries per thread in the level-0 accumulation: 64 at scale (~2^17+ lanes), fewer for
   // small inputs so the serial chain per lane stays short (a lone lane's madd ~12 us), and at
@@ -1422,11 +1517,20 @@ static size_t group_bytes(const MsmShape &s) {
   size_t cub = 0, cub2 = 0;
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(s.nmat() + 1)));
   ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)ns0));
+  if (s.s2) {
+    size_t cub3 = 0;
+    ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub3, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)(s.nmat2() + 1)));
+    if (cub3 > cub2) cub2 = cub3;
+  }
   size_t bytes = 0;
   auto add = [&](size_t b) { bytes += (b + 255) & ~size_t(255); };
   add(maxent * 4 * 3);                    // digits, level-1 values, list
   add(maxent * 2);                        // level-1 fine indices
   add((s.nmat() + 1) * 4 * 2);            // level-1 counts, their scan
+  if (s.s2) {
+    add(maxent * 2);                      // level-1.5 fine indices (values reuse the digits' buffer)
+    add((s.nmat2() + 1) * 4 * 2);         // level-1.5 counts, their scan
+  }
   add(s.NS * (nb + 1) * 4);               // offsets (every split)
   add(nb);                                // filled flags (split pipelines)
   add(ns0 * (xw + 4) + ns0 * 16 + 64);    // level-0 items, compacted keys + index, flags, pos, count
@@ -1508,7 +1612,8 @@ struct GroupPass {
   hipStream_t st;
   size_t nb, xw, maxent, ns0, ns1, cub = 0;
   uint32_t *list, *dig, *tmpv, *cnt, *coff, *offsets, *ikeys0, *ivals0, *ckeys, *cidx, *flags, *pos, *ccount;
-  uint16_t *tmpf;
+  uint16_t *tmpf, *tmpf2 = nullptr;
+  uint32_t *cnt2 = nullptr, *coff2 = nullptr;
   uint32_t *okA, *ovA, *okB, *ovB, *buckets, *Y;
   void *cubtmp;
   uint8_t *filled = nullptr;  // split pipelines: bucket b holds a sum from an earlier split
@@ -1539,6 +1644,11 @@ struct GroupPass {
     tmpf = dev.arena.take<uint16_t>(maxent);  // level-1 order: fine bucket within the coarse bin
     cnt = dev.arena.take<uint32_t>(s.nmat() + 1);
     coff = dev.arena.take<uint32_t>(s.nmat() + 1);
+    if (s.s2) {
+      tmpf2 = dev.arena.take<uint16_t>(maxent);
+      cnt2 = dev.arena.take<uint32_t>(s.nmat2() + 1);
+      coff2 = dev.arena.take<uint32_t>(s.nmat2() + 1);
+    }
     offsets = dev.arena.take<uint32_t>((size_t)s.NS * (nb + 1));  // split h: offsets + h (nb + 1)
     if (s.NS > 1) filled = dev.arena.take<uint8_t>(nb);
     ns0 = stitch_slots0(s);
@@ -1560,6 +1670,11 @@ struct GroupPass {
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, cnt, coff, (int)(s.nmat() + 1), st));
     ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub2, flags, pos, (int)ns0, st));
     if (cub2 > cub) cub = cub2;
+    if (s.s2) {
+      size_t cub3 = 0;
+      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub3, cnt2, coff2, (int)(s.nmat2() + 1), st));
+      if (cub3 > cub) cub = cub3;
+    }
     cubtmp = dev.arena.take<char>(cub);
     if (s.NS > 1) cubtmp_sort = dev.arena.take<char>(cub);
   }
@@ -1586,19 +1701,43 @@ struct GroupPass {
     hipLaunchKernelGGL(k_coarse<true>, grid, dim3(256), 0, st, dig, n, lo, hi, s.M, s.fs, s.nbins, coff, tmpv + base,
                        tmpf + base);
     ZK_CHECK(hipGetLastError());
-    const int cap = fine_stage_cap(s.fs);
-    const int lds = (4 << s.fs) + 4 * cap;
-    const uint32_t nq = (uint32_t)(s.W * s.nbins);
-    if ((size_t)(hi - lo) >= (size_t)s.nbins * 4096) {  // bins of >= 4096 entries: the wide workgroup
+    // level 1.5 when the coarse bins outgrow level 2's staging: sub-bins of this split's region
+    // (values into the digits' buffer, dead after level 1; the sorts of later splits follow on the
+    // same stream, so their digits are written only after this split's level 2 has read it)
+    const uint32_t *fv = tmpv + base, *fcoff = coff;
+    const uint16_t *ff = tmpf + base;
+    int fnwg = s.nwg, fs = s.fs;
+    uint32_t nq = (uint32_t)(s.W * s.nbins);
+    if (s.s2) {
+      const int nsub = 1 << s.s2, s2sh = s.fs - s.s2;
+      const dim3 g2((unsigned)s.nwg2, nq);
+      hipLaunchKernelGGL(k_split<false>, g2, dim3(256), 0, st, coff, s.nwg, s2sh, nsub, cnt2, tmpv + base, tmpf + base,
+                         dig + base, tmpf2 + base);
+      ZK_CHECK(hipGetLastError());
+      size_t cb2 = cub;
+      ZK_CHECK(hipcub::DeviceScan::ExclusiveSum(cubtmp, cb2, cnt2, coff2, (int)(s.nmat2() + 1), st));
+      hipLaunchKernelGGL(k_split<true>, g2, dim3(256), 0, st, coff, s.nwg, s2sh, nsub, coff2, tmpv + base, tmpf + base,
+                         dig + base, tmpf2 + base);
+      ZK_CHECK(hipGetLastError());
+      fv = dig + base;
+      ff = tmpf2 + base;
+      fcoff = coff2;
+      fnwg = s.nwg2;
+      fs = s2sh;
+      nq *= (uint32_t)nsub;
+    }
+    const int cap = fine_stage_cap(fs);
+    const int lds = (4 << fs) + 4 * cap;
+    if ((size_t)(hi - lo) * s.W >= (size_t)nq * 4096) {  // bins of >= 4096 entries: the wide workgroup
       ZK_CHECK(hipFuncSetAttribute((const void *)k_fine<1024, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    lds));
-      hipLaunchKernelGGL((k_fine<1024, 4, true>), dim3(nq), dim3(1024), lds, st, coff, s.nwg, nq, s.fs, cap,
-                         tmpv + base, tmpf + base, list + base, offsets + (size_t)sp * (nb + 1), base);
+      hipLaunchKernelGGL((k_fine<1024, 4, true>), dim3(nq), dim3(1024), lds, st, fcoff, fnwg, nq, fs, cap, fv, ff,
+                         list + base, offsets + (size_t)sp * (nb + 1), base);
     } else {
       ZK_CHECK(hipFuncSetAttribute((const void *)k_fine<256, 1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    lds));
-      hipLaunchKernelGGL((k_fine<256, 1, false>), dim3(nq), dim3(256), lds, st, coff, s.nwg, nq, s.fs, cap,
-                         tmpv + base, tmpf + base, list + base, offsets + (size_t)sp * (nb + 1), base);
+      hipLaunchKernelGGL((k_fine<256, 1, false>), dim3(nq), dim3(256), lds, st, fcoff, fnwg, nq, fs, cap, fv, ff,
+                         list + base, offsets + (size_t)sp * (nb + 1), base);
     }
     ZK_CHECK(hipGetLastError());
     if (st == this->st) mark("sort");

@@ -261,7 +261,7 @@ def main():
 
     ms_per_step = step_s * 1e3
     value = n_total / step_s
-    c = args.window if args.window else zk.load().zkg_msm_default_window(n_local)
+    c = args.window if args.window else zk.load().zkg_msm_window(zk.CURVE_ID[curve], n_local, 4, 1)
     accum_s = dist.max((kt_ms / kt_n) / 1e3 if kt_n else float("nan"))
 
     # parity of the timed result against the reference's own output (tests/golden)
@@ -425,7 +425,7 @@ def bench_config5(zk, args, dist):
     d_p.free()
     cfg = baseline().get("config5_bls12_381_msm_2^26")
     parity = ([int(x) for x in aff] == cfg["affine"]) if cfg and cfg["seed"] == seed and cfg["log_n"] == log_n else None
-    c = zk.load().zkg_msm_default_window(hi - lo)
+    c = zk.load().zkg_msm_window(zk.CURVE_ID["bls12_381"], hi - lo, 4, 1)
     out = {"workload": f"bls12_381_g1_msm_2^26_sharded{world}", "unit": "pairs/s", "value": n_total / step_s,
            "ms": step_s * 1e3, "n_gpus": world, "scaling": "strong (2^26 pairs in total at every N)",
            "pairs_per_gpu_max": hi - lo, "steps": args.config5_steps, "warmup": 1, "window_c": c,
@@ -512,7 +512,7 @@ def bench_config4(zk, steps=3, warmup=1):
     d_s.free()
     d_p.free()
     return {"workload": "bn128_g1_msm_2^24", "unit": "pairs/s", "value": n / dt, "ms": dt * 1e3, "steps": steps,
-            "warmup": warmup, "window_c": zk.load().zkg_msm_default_window(n), "parity_vs_reference": parity,
+            "warmup": warmup, "window_c": zk.load().zkg_msm_window(zk.CURVE_ID[curve], n, 4, 1), "parity_vs_reference": parity,
             "input_gen_s": gen_s}
 
 

@@ -304,6 +304,10 @@ ZKG_API void zkg_fft_generator(int curve, int m, uint64_t *out);
 
 /* MSM window heuristic used when window_size is not given */
 ZKG_API int zkg_msm_default_window(int npoints);
+/* the window a G1 MSM of `npoints` pairs runs with by default on `curve` (ZKG_BN128 /
+ * ZKG_BLS12_381) for its scalar form (Montgomery Fr, or std integers of expo_nlimbs limbs):
+ * zkg_msm_default_window's table, made curve-aware where a full top window measured faster */
+ZKG_API int zkg_msm_window(int curve, int npoints, int expo_nlimbs, int expos_mont);
 
 /* per-phase HIP-event profile of every MSM call, printed to stderr (diagnostics) */
 ZKG_API void zkg_msm_profile(int on);

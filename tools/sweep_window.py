@@ -32,7 +32,7 @@ def run(curve, logn, windows, reps=5, profile=False):
         dt = (time.perf_counter() - t) / reps
         kms, kn = zk.timer(enable=False)
         zk.msm_profile(False)
-        print(f"{curve} 2^{logn} c={c or zk.load().zkg_msm_default_window(n)}: {dt*1e3:.3f} ms/msm "
+        print(f"{curve} 2^{logn} c={c or zk.load().zkg_msm_window(zk.CURVE_ID[curve], n, 4, 1)}: {dt*1e3:.3f} ms/msm "
               f"({n/dt:.3e} pairs/s), accum {kms/kn:.3f} ms", flush=True)
     ds.free()
     dp.free()

@@ -291,6 +291,10 @@ ZKG_API void zkg_fft_generator(int curve, int m, uint64_t *out) {
 }
 
 ZKG_API int zkg_msm_default_window(int npoints) { return zk::msm_default_window(npoints); }
+ZKG_API int zkg_msm_window(int curve, int npoints, int expo_nlimbs, int expos_mont) {
+  const int bits = expos_mont ? (curve == ZKG_BN128 ? 254 : 255) : 64 * (expo_nlimbs < 4 ? expo_nlimbs : 4);
+  return zk::msm_default_window_bits(npoints, bits);
+}
 
 ZKG_API void zkg_msm_profile(int on) { zk::msm_set_profile(on); }
 ZKG_API void zkg_msm_set_group_limit(size_t entries) { zk::msm_set_group_limit(entries); }

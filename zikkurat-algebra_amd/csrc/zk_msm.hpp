@@ -29,6 +29,7 @@ template <> struct HostOf<BLS381_G2> {
 };
 
 int msm_default_window(int n);
+int msm_default_window_bits(int n, int bits);  // G1: the window for `bits`-bit scalars (curve-aware)
 void msm_set_profile(int on);  // per-phase event timing of every MSM call, printed to stderr
 void msm_set_group_limit(size_t entries);  // test hook: max sorted entries per pipeline pass (0: default)
 int msm_last_groups_read();  // window groups of the most recent msm_run (degrade-path tests)

@@ -2054,8 +2054,9 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
     return;
   }
   const bool explicit_window = window >= 4 && window <= 24;
-  const int c = explicit_window ? window : msm_default_window(n);
   const int bits = sc_in.mont ? HostOf<C>::Fr::BITS : 64 * sc_in.nread;
+  const int c = explicit_window ? window
+                                : (xyzz_words<F>() <= 64 ? msm_default_window_bits(n, bits) : msm_default_window(n));
   // small inputs with the default window: bit jobs, no buckets (an explicit window -- the
   // reference's _variable entry -- always runs the bucket method it names)
   if (!explicit_window && n <= msm_bits_max()) {
@@ -2205,13 +2206,15 @@ size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int windo
   using F = typename C::Fp;
   if (n <= 0) return 0;
   const int nread = nl < 4 ? nl : 4;
+  const int nbits = mont ? HostOf<C>::Fr::BITS : 64 * nread;
   if (!(window >= 4 && window <= 24) && n <= msm_bits_max()) {  // the bit-job path (msm_run_bits)
-    const int nbits = mont ? HostOf<C>::Fr::BITS : 64 * nread;
     const size_t io = host_inputs ? (size_t)n * nl * 8 + (size_t)n * 2 * C::NP64 * 8 : 0;
     return io + (size_t)n * aff_words<F>() * 4 + (size_t)nbits * msm_bits_groups(n) * xyzz_words<F>() * 4 + 4 * 256;
   }
-  const int c = (window >= 4 && window <= 24) ? window : msm_default_window(n);
-  const int W = (mont ? HostOf<C>::Fr::BITS : 64 * nread) / c + 1;
+  const int c = (window >= 4 && window <= 24)
+                    ? window
+                    : (xyzz_words<F>() <= 64 ? msm_default_window_bits(n, nbits) : msm_default_window(n));
+  const int W = nbits / c + 1;
   const int g = groups < 1 ? 1 : (groups > W ? W : groups);
   const int Wg = (W + g - 1) / g;
   const size_t sc_bytes = host_inputs ? (size_t)n * nl * 8 : 0;

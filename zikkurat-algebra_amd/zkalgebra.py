@@ -56,7 +56,7 @@ EXTENSION_SYMBOLS = [
     "zkg_version", "zkg_device_count", "zkg_set_device", "zkg_device_malloc", "zkg_device_free",
     "zkg_memcpy_htod", "zkg_memcpy_dtoh", "zkg_device_synchronize", "zkg_g1_msm_device", "zkg_ntt_device",
     "zkg_g1_proj_add", "zkg_g1_proj_normalize", "zkg_g1_proj_to_affine", "zkg_gen_fr", "zkg_gen_g1_points",
-    "zkg_fft_generator", "zkg_msm_default_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
+    "zkg_fft_generator", "zkg_msm_default_window", "zkg_msm_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
     "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
     "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
     "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_ntt_set_max_radix", "zkg_ntt_set_table_max",

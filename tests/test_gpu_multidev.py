@@ -68,10 +68,12 @@ def test_sharded_golden(gpu, curve, shards):
         assert np.array_equal(got, projn), name
 
 
-@pytest.mark.parametrize("shards", [2, 8], indirect=True)
+@pytest.mark.parametrize("shards", [2, 4, 8], indirect=True)
 def test_sharded_config5_2_26(gpu, shards):
     """BASELINE config 5 (2^26 BLS12-381 pairs) through bls12_381_G1_proj_MSM_mont_coeff_affine_out
-    with the device set: equal to the reference's output"""
+    with the device set: equal to the reference's output (chunks of 2^25 / 2^24 / 2^23 pairs -- the
+    per-GPU sizes of the multi-GPU config-5 line at N = 2 / 4 / 8, c = 20 with the sub-bin sort at
+    the first two)"""
     cfg = baseline_configs().get("config5_bls12_381_msm_2^26")
     if cfg is None:
         pytest.skip("config 5 missing")

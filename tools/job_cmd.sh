@@ -1,9 +1,5 @@
-# r04za: BN128 c = 16 vs 17 at 2^19..2^24; BLS12-381 c = 16 vs 20 at 2^22..2^24
+# r04zc: kernel stats of BLS12-381 2^26 MSMs with the sub-bin sort
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-for lg in 19 20 21 22 23 24; do
-  timeout -k 10 200 python -u tools/sweep_window.py bn128 $lg 16 17 2>&1 | grep -v amdgpu.ids || exit 1
-done
-for lg in 22 23 24; do
-  timeout -k 10 300 python -u tools/sweep_window.py bls12_381 $lg 16 20 2>&1 | grep -v amdgpu.ids || exit 1
-done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04zc_p26 -o run --output-format csv -- python3 tools/sweep_window.py bls12_381 26 20 > gpurun_out/r04zc_p26.log 2>&1 || exit 1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_multidev.py -m gpu -k "config5" 2>&1 | tail -2 || exit 1

@@ -415,7 +415,7 @@ __device__ __forceinline__ void xyzz_scl(Xyzz<F> &r, const Xyzz<F> &P, const uin
 #include "zk_glv.inc"
 
 struct GlvParams {  // decomposition constants of one curve (kernel argument)
-  uint64_t g1[4], g2[4], a1[3], b1[3], a2[3], b2[3], lambda[3];
+  uint64_t g1[4], g2[4], a1[3], b1[3], a2[3], b2[3];
   int s1, s2;
 };
 template <class C>
@@ -425,12 +425,10 @@ static GlvParams glv_params() {
   if constexpr (C::NP64 == 4) {
     cp(p.g1, GLV_BN254_G1, 4); cp(p.g2, GLV_BN254_G2, 4);
     cp(p.a1, GLV_BN254_A1, 3); cp(p.b1, GLV_BN254_B1, 3); cp(p.a2, GLV_BN254_A2, 3); cp(p.b2, GLV_BN254_B2, 3);
-    cp(p.lambda, GLV_BN254_LAMBDA, 3);
     p.s1 = GLV_BN254_SGN1; p.s2 = GLV_BN254_SGN2;
   } else {
     cp(p.g1, GLV_BLS381_G1, 4); cp(p.g2, GLV_BLS381_G2, 4);
     cp(p.a1, GLV_BLS381_A1, 3); cp(p.b1, GLV_BLS381_B1, 3); cp(p.a2, GLV_BLS381_A2, 3); cp(p.b2, GLV_BLS381_B2, 3);
-    cp(p.lambda, GLV_BLS381_LAMBDA, 3);
     p.s1 = GLV_BLS381_SGN1; p.s2 = GLV_BLS381_SGN2;
   }
   return p;
@@ -791,8 +789,7 @@ __device__ __forceinline__ void jac_mul_absz(Jac<F> &r, const Jac<F> &p) {
 // 128 bits on BLS12-381; tools/gen_glv.py checks the test on subgroup and non-subgroup points).
 // bad[block] = 1 when some point of the block fails.
 template <class C>
-__global__ void __launch_bounds__(256) k_subgroup_check(int n, const uint32_t *__restrict__ A, GlvParams gp,
-                                                        W6 beta_ref, uint32_t *__restrict__ scratch, int lanes,
+__global__ void __launch_bounds__(256) k_subgroup_check(int n, const uint32_t *__restrict__ A, W6 beta_ref, int lanes,
                                                         uint32_t *__restrict__ bad) {
   using F = typename C::Fp;
   Fe<F> beta, t0;
@@ -1048,8 +1045,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   const W6 beta = glv_beta_ref<C>();
   if (glv && C::NP64 == 6) {
     const unsigned grid = (unsigned)(glanes / 256);
-    hipLaunchKernelGGL(k_subgroup_check<C>, dim3(grid), dim3(256), 0, st, (int)N, A, gp, beta, scratch, (int)glanes,
-                       bad);
+    hipLaunchKernelGGL(k_subgroup_check<C>, dim3(grid), dim3(256), 0, st, (int)N, A, beta, (int)glanes, bad);
     ZK_CHECK(hipGetLastError());
     uint32_t *hb = reinterpret_cast<uint32_t *>(dev.host_staging(grid * 4 + 64));
     ZK_CHECK(hipMemcpyAsync(hb, bad, grid * 4, hipMemcpyDeviceToHost, st));

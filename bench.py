@@ -162,6 +162,15 @@ class Dist:
                 from sharded import LibComm
                 self.comm = LibComm(self.rank, self.world)
 
+    def world_seen(self):
+        """ranks the exchange actually connects (the library's communicator / the gloo group)"""
+        if self.comm:
+            import zkalgebra as zk
+            return int(zk.load().zkg_comm_world())
+        if self.dist:
+            return int(self.dist.get_world_size())
+        return 1
+
     def barrier(self):
         if self.comm:
             self.comm.barrier()
@@ -225,8 +234,112 @@ def timed(dist, step, steps, warmup, sync, zk=None):
     return dist.max(time.perf_counter() - t0) / steps, out
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, script=None, grace_s=10.0):
+    """Launcher of `bench.py --gpus N` run without torchrun (no WORLD_SIZE in the environment):
+    start N fresh rank processes of `script` (this file) with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT and one rendezvous key + nonce for the launch, forward rank 0's
+    stdout (the JSON line) and return a non-zero code if any rank fails -- the other ranks are then
+    terminated (by their own pids), so a rank blocked in a collective cannot hang the launch.
+    The launcher itself never imports the library or torch and makes no GPU call: every HIP
+    runtime lives in a rank process."""
+    import signal
+    import subprocess
+    import threading
+    import uuid
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    nonce = uuid.uuid4().hex
+    procs = []
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except OSError:
+                    pass
+
+    def on_signal(signum, _frame):
+        stop_all()
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    lines = []
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       ZKG_RDZV_KEY=f"bench_{os.getpid()}_{port}", ZKG_RDZV_NONCE=nonce)
+            procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
+                                          stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                          text=True))
+
+        def pump():  # rank 0's stdout, line by line, to ours
+            for line in procs[0].stdout:
+                lines.append(line)
+                sys.stdout.write(line)
+                sys.stdout.flush()
+
+        t = threading.Thread(target=pump, daemon=True)
+        t.start()
+        rc = 0
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                rc = bad[0][1]
+                r = bad[0][0]
+                print(f"[bench launcher] rank {r} exited with {rc}; stopping the other ranks", file=sys.stderr, flush=True)
+                stop_all()
+                t_end = time.time() + grace_s
+                while time.time() < t_end and any(p.poll() is None for p in procs):
+                    time.sleep(0.05)
+                stop_all(signal.SIGKILL)
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.05)
+        for p in procs:
+            p.wait()
+        t.join(timeout=5)
+        if rc == 0 and not any(line.lstrip().startswith("{") for line in lines):
+            print("[bench launcher] rank 0 printed no result line", file=sys.stderr, flush=True)
+            rc = 1
+        return rc if rc >= 0 else 128 - rc  # a rank killed by signal k -> 128 + k
+    finally:
+        stop_all(signal.SIGKILL)
+        for s, h in old.items():
+            signal.signal(s, h)
+
+
+def check_world(args):
+    """--gpus N is the world the caller asked for: under an external launcher (WORLD_SIZE set) it
+    must match WORLD_SIZE, or the run would report a world it was not asked for.  Returns the
+    error message, or None."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is not None and int(env) != args.gpus:
+        return f"--gpus {args.gpus} but the launcher started WORLD_SIZE={env} ranks"
+    return None
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no external launcher: this process only starts the N ranks (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    err = check_world(args)
+    if err:
+        print(f"[bench] {err}", file=sys.stderr, flush=True)
+        sys.exit(2)
     import numpy as np
     import zkalgebra as zk
     from sharded import shard_range
@@ -237,6 +350,10 @@ def main():
     zk.load().zkg_set_device(device)
     dist = Dist(args, device)
     world, rank = dist.world, dist.rank
+    if dist.world_seen() != args.gpus:
+        print(f"[bench] rank {rank}: the communicator holds {dist.world_seen()} ranks, --gpus asked for {args.gpus}",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
 
     curve = args.curve
     log_n = args.log_n

@@ -7,6 +7,64 @@ import numpy as np
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+P_BLS = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+FP_ID = {"bn128": 0, "bls12_381": 2}  # oracle field ids of the base fields
+
+
+def _limbs(x, n):
+    return np.array([(x >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(n)], dtype=np.uint64)
+
+
+def projective_points(zk, oracle, curve, n, seed, n_inf=3):
+    """n projective points (X:Y:Z) = (x l : y l : l) of the order-r subgroup with random l (the
+    generator's points scaled by random field elements), a few at infinity as (0 : l : 0).
+    Deterministic: the same rows here, in the GPU tests and in tools/make_golden.py."""
+    import ctypes
+    import random
+
+    def ptr(a):
+        return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    NP = zk.NLIMBS_P[curve]
+    aff = zk.gen_points(curve, seed, n)
+    lam = zk.gen_points(curve, seed + 1, n)[:, :NP]  # random field elements (canonical)
+    out = np.zeros((n, 3 * NP), dtype=np.uint64)
+    for i in range(n):
+        for k in range(2):
+            x = np.ascontiguousarray(aff[i, k * NP:(k + 1) * NP])
+            o = np.zeros(NP, dtype=np.uint64)
+            oracle.lib.zko_fmul(FP_ID[curve], ptr(x), ptr(np.ascontiguousarray(lam[i])), ptr(o))
+            out[i, k * NP:(k + 1) * NP] = o
+        out[i, 2 * NP:] = lam[i]
+    rng = random.Random(seed)
+    for i in rng.sample(range(n), min(n_inf, n)):
+        out[i] = 0
+        out[i, NP:2 * NP] = lam[i]  # (0 : y : 0) with arbitrary y is infinity too
+    return out
+
+
+def bls_nonsubgroup_points(n, seed):
+    """random affine points of E(Fp): y^2 = x^3 + 4, almost surely outside the order-r subgroup
+    (cofactor h ~ 2^126); Montgomery form (R = 2^384)"""
+    import random
+    rng = random.Random(seed)
+    R = 1 << 384
+    pts = []
+    while len(pts) < n:
+        x = rng.randrange(P_BLS)
+        rhs = (x * x * x + 4) % P_BLS
+        y = pow(rhs, (P_BLS + 1) // 4, P_BLS)
+        if y * y % P_BLS != rhs:
+            continue
+        pts.append(np.concatenate([_limbs(x * R % P_BLS, 6), _limbs(y * R % P_BLS, 6)]))
+    return np.stack(pts)
+
+
+def group_fft_golden():
+    """reference digests of the group FFT at KZG SRS sizes (tools/make_golden.py groupfft)"""
+    p = os.path.join(GOLD, "group_fft.json")
+    return json.load(open(p)) if os.path.exists(p) else {}
+
+
 def msm_cases(curve):
     z = np.load(os.path.join(GOLD, f"msm_{curve}.npz"), allow_pickle=False)
     for name in z["names"]:

@@ -41,10 +41,12 @@ class _FakeLib:
         return 0
 
 
-def _rank(rank, world, key, rdir, q):
+def _rank(rank, world, key, rdir, q, nonce=None):
     sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
     os.environ["ZKG_RDZV_KEY"] = key
     os.environ["ZKG_RDZV_DIR"] = rdir
+    if nonce:
+        os.environ["ZKG_RDZV_NONCE"] = nonce
     import sharded
     fake = _FakeLib(key, rdir)
     sharded.zk.load = lambda: fake
@@ -84,3 +86,47 @@ def test_rendezvous_path_default_key(monkeypatch):
     monkeypatch.setenv("MASTER_PORT", "29517")
     p = sharded.rendezvous_path()
     assert p.endswith(f"zkg_rdzv_{os.getppid()}_29517.id")
+
+
+def test_stale_id_of_an_earlier_launch_is_ignored(tmp_path):
+    """an id file left by an earlier launch with the same key (e.g. its rank 0 died) carries that
+    launch's nonce: a rank of the new launch that starts before the new rank 0 must wait for the
+    new id instead of joining the dead launch's communicator"""
+    key, stale = "launchS", os.urandom(128)
+    (tmp_path / f"zkg_rdzv_{key}.id").write_bytes(stale + b"old-launch")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    r1 = ctx.Process(target=_rank, args=(1, 2, key, str(tmp_path), q, "new-launch"))
+    r1.start()
+    time.sleep(1.0)  # rank 1 polls the stale file first
+    r0 = ctx.Process(target=_rank, args=(0, 2, key, str(tmp_path), q, "new-launch"))
+    r0.start()
+    got = [q.get(timeout=120)[1] for _ in range(2)]
+    for p in (r0, r1):
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][2] == got[1][2] != stale
+    assert not (tmp_path / f"zkg_rdzv_{key}.id").exists()
+
+
+def test_rank0_failed_init_removes_its_id(tmp_path, monkeypatch):
+    sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
+    import sharded
+    monkeypatch.setenv("ZKG_RDZV_KEY", "launchF")
+    monkeypatch.setenv("ZKG_RDZV_DIR", str(tmp_path))
+    fake = _FakeLib("launchF", str(tmp_path))
+    fake.zkg_comm_init = lambda rank, world, buf: -1
+    monkeypatch.setattr(sharded.zk, "load", lambda: fake)
+    with pytest.raises(RuntimeError, match="zkg_comm_init"):
+        sharded.LibComm(0, 2, timeout=5)
+    assert not (tmp_path / "zkg_rdzv_launchF.id").exists()
+
+
+def test_multi_rank_without_torchrun_or_key_fails_fast(monkeypatch):
+    sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
+    import sharded
+    for k in ("ZKG_RDZV_KEY", "TORCHELASTIC_RUN_ID"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(RuntimeError, match="ZKG_RDZV_KEY"):
+        sharded.rendezvous_path()

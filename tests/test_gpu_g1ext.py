@@ -5,58 +5,23 @@ reference-named C ABI, bit-exact against the reference's own C (oracle/_ref):
 Inputs: projective points with non-trivial Z, points at infinity, and (BLS12-381) points
 OUTSIDE the order-r subgroup -- for those the result depends on the exact per-level
 scalars, so they pin the per-level structure, not just the linear map mod r."""
-import random
+import hashlib
 
 import numpy as np
 import pytest
 
+import golden_io
+
 pytestmark = pytest.mark.gpu
 CURVES = ["bn128", "bls12_381"]
-FP = {"bn128": 0, "bls12_381": 2}
-P_BLS = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
-
-
-def to_limbs(x, n):
-    return np.array([(x >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(n)], dtype=np.uint64)
 
 
 def projective(gpu, oracle, curve, n, seed, n_inf=3):
-    """n projective points (X:Y:Z) = (x l : y l : l) with random l, a few at infinity"""
-    NP = gpu.NLIMBS_P[curve]
-    aff = gpu.gen_points(curve, seed, n)
-    lam = gpu.gen_points(curve, seed + 1, n)[:, :NP]  # random field elements (canonical)
-    out = np.zeros((n, 3 * NP), dtype=np.uint64)
-    for i in range(n):
-        for k in range(2):
-            oracle.lib.zko_fmul(FP[curve], _p(aff[i, k * NP:(k + 1) * NP]), _p(lam[i]),
-                                _p(out[i, k * NP:(k + 1) * NP]))
-        out[i, 2 * NP:] = lam[i]
-    rng = random.Random(seed)
-    for i in rng.sample(range(n), min(n_inf, n)):
-        out[i] = 0
-        out[i, NP:2 * NP] = lam[i]  # (0 : y : 0) with arbitrary y is infinity too
-    return out
-
-
-def _p(a):
-    import ctypes
-    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    return golden_io.projective_points(gpu, oracle, curve, n, seed, n_inf)
 
 
 def bls_nonsubgroup_points(n, seed):
-    """random points of E(Fp): y^2 = x^3 + 4, almost surely outside the order-r subgroup
-    (cofactor h ~ 2^126); Montgomery form (R = 2^384)"""
-    rng = random.Random(seed)
-    R = 1 << 384
-    pts = []
-    while len(pts) < n:
-        x = rng.randrange(P_BLS)
-        rhs = (x * x * x + 4) % P_BLS
-        y = pow(rhs, (P_BLS + 1) // 4, P_BLS)
-        if y * y % P_BLS != rhs:
-            continue
-        pts.append(np.concatenate([to_limbs(x * R % P_BLS, 6), to_limbs(y * R % P_BLS, 6)]))
-    return np.stack(pts)
+    return golden_io.bls_nonsubgroup_points(n, seed)
 
 
 def ref_call(reference, curve, name, *args):
@@ -140,3 +105,33 @@ def test_fft_roundtrip_2_12(gpu, curve):
     sg = gpu.get_fft_subgroup(curve, m)
     back = gpu.inverse_fft(sg, gpu.forward_fft(sg, proj))
     assert np.array_equal(back, proj)
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+GFFT = golden_io.group_fft_golden()
+
+
+@pytest.mark.parametrize("key", sorted(GFFT))
+def test_fft_vs_reference_digests(gpu, oracle, key):
+    """KZG-SRS sizes (the reference's curveIFFT builds the Lagrange SRS with fft_inverse,
+    examples/KZG.hs:55): 2^12 and 2^14 subgroup points with random Z and infinities on both curves
+    (the GLV stages at full occupancy, the 4-lane first inverse stage, shared-table lane pairs),
+    and BLS12-381 points outside the r-subgroup at 2^10 (the integer stages).  The reference's
+    outputs are stored as SHA-256 digests (tools/make_golden.py groupfft)."""
+    g = GFFT[key]
+    curve, m, kind = g["curve"], g["log_n"], g["input"]
+    n = 1 << m
+    if kind == "subgroup_projective":
+        pts = projective(gpu, oracle, curve, n, g["seed"], n_inf=g["n_inf"])
+    else:
+        pts = gpu.batch_from_affine(curve, bls_nonsubgroup_points(n, g["seed"]))
+    assert _sha(pts) == g["input_sha256"]
+    sg = gpu.get_fft_subgroup(curve, m)
+    fwd = gpu.forward_fft(sg, pts)
+    assert gpu.g1_fft_last_glv() == (1 if kind == "subgroup_projective" else 0)
+    assert _sha(fwd) == g["forward_sha256"], key
+    inv = gpu.inverse_fft(sg, pts)
+    assert _sha(inv) == g["inverse_sha256"], key

@@ -9,6 +9,10 @@
 #   smoke     __graft_entry__.smoke()             -> gpurun_out/TAG_smoke.log
 #   bench     python bench.py (defaults)          -> gpurun_out/TAG_bench.json
 #   bench2    bench.py as 2 ranks on the one GPU (gloo exchange) -> gpurun_out/TAG_bench2.json
+#   bench2self  bench.py --gpus 2 started WITHOUT torchrun (bench.py's own launcher), gloo exchange
+#             -> gpurun_out/TAG_bench2self.json (must print n_gpus 2 and config5 parity true)
+#   bench2rccl  bench.py --gpus 2 with the RCCL backend on the one GPU: RCCL refuses two ranks on one
+#             device, so the launch MUST exit non-zero (no world-1 line) -> gpurun_out/TAG_bench2rccl.*
 #   prof      rocprofv3 --kernel-trace --stats of a short bench -> gpurun_out/TAG_prof/
 #   pmcf      rocprofv3 --pmc FETCH_SIZE (own pass) -> gpurun_out/TAG_pmcf/
 #   pmcw      rocprofv3 --pmc WRITE_SIZE (own pass) -> gpurun_out/TAG_pmcw/
@@ -41,6 +45,12 @@ for step in "$@"; do
     bench) timeout -k 10 400 python -u bench.py > ${O}_bench.json 2> ${O}_bench.err ;;
     bench2) timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
               --master-port 29517 bench.py --gpus 2 --backend gloo --steps 3 --warmup 1 > ${O}_bench2.json 2> ${O}_bench2.err ;;
+    bench2self) timeout -k 10 600 python -u bench.py --gpus 2 --backend gloo --no-extras --no-e2e --no-cpu-baseline \
+              --no-config4 --steps 5 --warmup 1 > ${O}_bench2self.json 2> ${O}_bench2self.err ;;
+    bench2rccl) timeout -k 10 300 python -u bench.py --gpus 2 --no-extras --no-e2e --no-cpu-baseline --no-config4 \
+              --no-config5 --no-ntt --steps 2 --warmup 1 > ${O}_bench2rccl.json 2> ${O}_bench2rccl.err
+              rc=$?; echo "bench2rccl rc=$rc (non-zero expected)" >> ${O}_bench2rccl.err
+              [ $rc -ne 0 ] && [ $rc -ne 124 ] && [ $rc -ne 137 ] && [ ! -s ${O}_bench2rccl.json ]; (exit $?) ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d ${O}_prof -o run --output-format csv -- python3 $BENCH_SHORT \
               > ${O}_prof_bench.json 2> ${O}_prof.err ;;
     pmcf) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d ${O}_pmcf -o run --output-format csv -- python3 $BENCH_SHORT \

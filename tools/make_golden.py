@@ -10,6 +10,10 @@ independent restatement in oracle/zk_oracle.c is checked equal by the tests).
 
   python tools/make_golden.py small     # edge-case MSM + NTT vectors (stored in full)  ~1 min
   python tools/make_golden.py large     # BASELINE-config outputs / SHA-256 digests     ~10 min, 8 cores
+  python tools/make_golden.py groupfft  # group FFT at KZG SRS sizes (m = 12, 14, both curves, subgroup
+                                        # points with random Z; BLS12-381 non-subgroup points at m = 10):
+                                        # reference forward / inverse SHA-256 digests
+                                        # -> tests/golden/group_fft.json      ~1 min, 8 cores
   python tools/make_golden.py patterns  # adversarial NTT inputs (tests/golden_io.py NTT_PATTERNS) at
                                         # m = 5, 12, 14, 20 and random 2^20 vectors: reference forward /
                                         # inverse SHA-256 digests -> tests/golden/ntt_patterns.json   ~1 min
@@ -247,6 +251,60 @@ def large_ntt(curve, logn, seed):
             "roundtrip_ok": True, "reference_forward_seconds": tf, "reference_inverse_seconds": ti}
 
 
+# ----------------------------------------------------------------------------- group FFT
+
+GFFT_CASES = [  # (key, curve, m, input kind, seed, infinities)
+    ("bn128_m12", "bn128", 12, "subgroup_projective", 0x6F0012, 3),
+    ("bn128_m14", "bn128", 14, "subgroup_projective", 0x6F0014, 5),
+    ("bls12_381_m12", "bls12_381", 12, "subgroup_projective", 0x6F1012, 3),
+    ("bls12_381_m14", "bls12_381", 14, "subgroup_projective", 0x6F1014, 5),
+    ("bls12_381_nonsubgroup_m10", "bls12_381", 10, "nonsubgroup_affine", 0x6F200A, 0),
+]
+
+
+def _gfft_input(case):
+    _, curve, m, kind, seed, n_inf = case
+    n = 1 << m
+    if kind == "subgroup_projective":
+        return golden_io.projective_points(zk, Oracle(), curve, n, seed, n_inf=n_inf)
+    aff = golden_io.bls_nonsubgroup_points(n, seed)
+    out = np.zeros((n, 3 * zk.NLIMBS_P[curve]), dtype=np.uint64)
+    Reference().arr(curve, "G1_proj_batch_from_affine", n, aff, out)
+    return out
+
+
+def _gfft_job(args):
+    case, inverse = args
+    key, curve, m = case[:3]
+    pts = _gfft_input(case)
+    g = zk.get_fft_subgroup(curve, m).gen_array()
+    out = np.zeros_like(pts)
+    t = time.time()
+    Reference().arr(curve, "G1_proj_fft_inverse" if inverse else "G1_proj_fft_forward", m, g, pts, out)
+    return key, inverse, sha(pts), sha(out), time.time() - t
+
+
+def make_group_fft():
+    os.makedirs(GOLD, exist_ok=True)
+    with mp.Pool(8) as pool:
+        res = pool.map(_gfft_job, [(c, inv) for c in GFFT_CASES for inv in (False, True)])
+    data = {}
+    for case in GFFT_CASES:
+        key, curve, m, kind, seed, n_inf = case
+        d = {"curve": curve, "log_n": m, "input": kind, "seed": seed, "n_inf": n_inf,
+             "reference": "<C>_G1_proj_fft_forward / _inverse of lib/cbits (bls12_381_G1_proj.c:679-790)"}
+        for k, inv, sin, sout, dt in res:
+            if k != key:
+                continue
+            d["input_sha256"] = sin
+            d["inverse_sha256" if inv else "forward_sha256"] = sout
+            d["reference_inverse_seconds" if inv else "reference_forward_seconds"] = dt
+        data[key] = d
+        print(key, "forward %.1fs inverse %.1fs" % (d["reference_forward_seconds"], d["reference_inverse_seconds"]),
+              flush=True)
+    json.dump(data, open(os.path.join(GOLD, "group_fft.json"), "w"), indent=1, sort_keys=True)
+
+
 def make_large(which):
     os.makedirs(GOLD, exist_ok=True)
     path = os.path.join(GOLD, "baseline_configs.json")
@@ -272,12 +330,14 @@ def make_large(which):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) < 2 or sys.argv[1] not in ("small", "large", "patterns"):
+    if len(sys.argv) < 2 or sys.argv[1] not in ("small", "large", "patterns", "groupfft"):
         print(__doc__)
         sys.exit(2)
     if sys.argv[1] == "small":
         make_small()
     elif sys.argv[1] == "patterns":
         make_patterns()
+    elif sys.argv[1] == "groupfft":
+        make_group_fft()
     else:
         make_large(sys.argv[2] if len(sys.argv) > 2 else None)

@@ -325,6 +325,7 @@ ZKG_API void zkg_release(void) {
   guard([&] {
   int prev = 0;
   ZK_CHECK(hipGetDevice(&prev));
+  DeviceGuard restore(prev);
   for (Device *d : all_devices()) {
     std::lock_guard<std::mutex> lock(d->mu);
     ZK_CHECK(hipSetDevice(d->id));
@@ -332,7 +333,6 @@ ZKG_API void zkg_release(void) {
     zk::ntt_release(*d);
     d->release_memory();
   }
-  ZK_CHECK(hipSetDevice(prev));
   });
 }
 

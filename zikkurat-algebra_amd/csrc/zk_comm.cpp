@@ -17,6 +17,7 @@
 #include <string.h>
 #include <unistd.h>
 #include <mutex>
+#include <string>
 #include <vector>
 #include "../../include/zkalgebra_gpu.h"
 #include "zk_host.hpp"
@@ -57,20 +58,6 @@ void grow(void *&p, size_t &cap, size_t bytes) {
   cap = bytes;
 }
 
-// the calling thread on the communicator's device while a guard lives
-struct OnCommDevice {
-  int prev = 0;
-  explicit OnCommDevice(int dev) {
-    ZK_CHECK(hipGetDevice(&prev));
-    if (prev != dev) ZK_CHECK(hipSetDevice(dev));
-  }
-  ~OnCommDevice() {
-    int cur = 0;
-    ZK_CHECK(hipGetDevice(&cur));
-    if (cur != prev) ZK_CHECK(hipSetDevice(prev));
-  }
-};
-
 // RCCL prints a version banner on stdout when it initialises; the caller's stdout is not ours
 // (bench.py's contract is one JSON line there), so stdout points at stderr while RCCL sets up
 struct StdoutToStderr {
@@ -92,7 +79,7 @@ struct StdoutToStderr {
 // ncclAllGather of `bytes` per rank from host `send` into host `recv` (world * bytes), through
 // device staging on the communicator device's library stream.  Caller holds g_comm.mu.
 int allgather_host(const void *send, void *recv, size_t bytes) {
-  OnCommDevice on(g_comm.device);
+  DeviceGuard on(g_comm.device);
   Device &dev = current_device();
   std::lock_guard<std::mutex> lock(dev.mu);
   grow(g_comm.d_send, g_comm.cap_send, bytes);
@@ -134,17 +121,34 @@ template <class C>
 int sharded_msm(int n, const uint64_t *d_expos, int nl, bool mont, const uint64_t *d_grps, int window, int shards,
                 uint64_t *tgt) {
   constexpr int NP = C::NP64;
-  std::vector<uint64_t> mine((size_t)shards * 3 * NP), all((size_t)shards * g_comm.world * 3 * NP);
-  {
-    OnCommDevice on(g_comm.device);
+  // payload per rank: the `shards` partials and one status word (non-zero: this rank's chunk
+  // failed).  A rank whose chunk MSM throws (recoverable error mode, e.g. out of device memory)
+  // still takes part in the all-gather, so its peers are not left waiting in the collective; then
+  // every rank returns an error.
+  const size_t per = (size_t)shards * 3 * NP + 1;
+  std::vector<uint64_t> mine(per, 0), all(per * (size_t)g_comm.world);
+  std::string local_err;
+  try {
+    DeviceGuard on(g_comm.device);
     for (int k = 0; k < shards; k++) {  // the rank's chunk as `shards` contiguous sub-chunks
       const size_t lo = (size_t)n * k / shards, hi = (size_t)n * (k + 1) / shards;
       msm_g1<C>((int)(hi - lo), d_expos + lo * nl, nl, d_grps + lo * 2 * NP, /*host_inputs=*/false, mont, window,
                 mine.data() + (size_t)k * 3 * NP);
     }
+  } catch (const Error &e) {
+    local_err = e.what();
+    mine[per - 1] = 1;
   }
-  if (int e = allgather_host(mine.data(), all.data(), mine.size() * 8)) return e;
-  sum_partials<C>(all.data(), shards * g_comm.world, tgt);
+  if (int e = allgather_host(mine.data(), all.data(), per * 8)) return e;
+  for (int r = 0; r < g_comm.world; r++)
+    if (all[(size_t)r * per + per - 1]) {
+      if (!local_err.empty()) throw Error(local_err);
+      throw Error("zkg_g1_msm_device_sharded: rank " + std::to_string(r) + " failed its chunk MSM");
+    }
+  std::vector<uint64_t> parts((size_t)shards * g_comm.world * 3 * NP);
+  for (int r = 0; r < g_comm.world; r++)
+    memcpy(parts.data() + (size_t)r * shards * 3 * NP, all.data() + (size_t)r * per, (size_t)shards * 3 * NP * 8);
+  sum_partials<C>(parts.data(), shards * g_comm.world, tgt);
   return 0;
 }
 
@@ -204,7 +208,7 @@ ZKG_API int zkg_comm_destroy(void) {
   return guard_ret(-3, [&]() -> int {
   std::lock_guard<std::mutex> lock(g_comm.mu);
   if (!g_comm.comm) return 0;
-  OnCommDevice on(g_comm.device);
+  DeviceGuard on(g_comm.device);
   {
     Device &dev = current_device();
     std::lock_guard<std::mutex> dlock(dev.mu);

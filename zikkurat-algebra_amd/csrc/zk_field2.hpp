@@ -23,6 +23,19 @@ struct F2 {
   static constexpr int RB = B::RB;
 };
 
+// G1 (base field) or G2 (Fp2) point coordinates: the paths tuned and measured on G1 only (the
+// curve-aware window table, the quad-cooperative stitch and Y-sum fold) gate on this
+template <class F>
+struct IsF2 {
+  static constexpr bool value = false;
+};
+template <class B>
+struct IsF2<F2<B>> {
+  static constexpr bool value = true;
+};
+template <class F>
+constexpr bool is_base_field() { return !IsF2<F>::value; }
+
 template <class B>
 __device__ __forceinline__ void f2_split(Fe<B> &c0, Fe<B> &c1, const Fe<F2<B>> &a) {
 #pragma unroll

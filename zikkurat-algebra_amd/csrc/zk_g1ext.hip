@@ -332,8 +332,18 @@ __device__ __forceinline__ uint32_t win5(const uint64_t *K, int i) {
   if (o > 59 && w < 4) v |= K[w + 1] << (64 - o);
   return (uint32_t)v & 31u;
 }
+// Every point routine of the group FFT is inlined into its kernel.  Round 4's first Jacobian
+// build left xyzz_scl outlined (a real call: s_swappc_b64 into it, s_setpc_b64 s[30:31] back), and
+// LLVM's branch relaxation of a long branch inside the callee took s[30:31] -- the return address
+// -- as its scratch pair without saving it, so the return jumped into the callee's own body and
+// the kernel never finished (profiles/r05*_fft_outlined_scl.txt holds the disassembly of that
+// variant, built with -DZK_FFT_SCL_ATTR=__noinline__).  tests/test_isa_guard.py checks the
+// shipped code object: no group-FFT kernel may contain a call.
+#ifndef ZK_FFT_SCL_ATTR
+#define ZK_FFT_SCL_ATTR __forceinline__
+#endif
 template <class F>
-__device__ __forceinline__ void xyzz_scl(Xyzz<F> &r, const Xyzz<F> &P, const uint64_t *k, uint32_t *__restrict__ tab) {
+__device__ ZK_FFT_SCL_ATTR void xyzz_scl(Xyzz<F> &r, const Xyzz<F> &P, const uint64_t *k, uint32_t *__restrict__ tab) {
   if (xyzz_is_inf(P)) {
     r = P;
     return;

@@ -1070,7 +1070,7 @@ __global__ void __launch_bounds__(256, ZK_YSUM_WAVES) k_ysum2(const uint32_t *__
   constexpr int XW = xyzz_words<F>();
   // G1: the fold runs quad-cooperatively (2 x 64 KB of LDS for BLS12-381: the parked sums and
   // xyzz_add_quad's per-lane doubling fallback); Fp2 points keep the one-lane fold (LDS)
-  constexpr bool QUAD_FOLD = ZK_YSUM_QUAD_FOLD && XW <= 64;
+  constexpr bool QUAD_FOLD = ZK_YSUM_QUAD_FOLD && is_base_field<F>();
   __shared__ uint4 park4[(QUAD_FOLD ? 256 : 128) * XW / 4];
   __shared__ uint4 fold4[QUAD_FOLD ? 256 * XW / 4 : 1];
   uint32_t *park = reinterpret_cast<uint32_t *>(park4);
@@ -1161,6 +1161,101 @@ __global__ void __launch_bounds__(256, ZK_YSUM_WAVES) k_ysum2(const uint32_t *__
   }
 }
 
+// 6''. k_ysum3: k_ysum2 at TWO waves per SIMD, for the large windows (c = 20 at 2^23-2^26:
+//      W * 2^c = 13.6M bucket additions, ~13 block rounds of k_ysum2 at one wave per SIMD, where
+//      that kernel issues only ~0.6 of the VALU slots: nothing hides a lone wave's product and
+//      load latencies).  The next bucket is gathered straight into LDS by global_load_lds while
+//      the current addition runs (as in k_accum), so the prefetch costs no VGPRs (k_ysum2's
+//      register prefetch holds 288); the block fold reuses the same LDS image after the loop
+//      (one-lane additions: the fold is ~6 % of the additions at 16 buckets per lane).  64 KB of
+//      LDS per block at BLS12-381: two blocks per CU.  G1 only.  (At BLS12-381 2^20 there are
+//      65536 Y-sum lanes, one wave per SIMD in total, so this shape would only halve the lanes'
+//      work and add fold levels: measured 0.36-0.39 vs 0.32 ms there, profiles/r03i_*.)
+template <class C>
+__global__ void __launch_bounds__(256, 2) k_ysum3(const uint32_t *__restrict__ buckets,
+                                                  const uint32_t *__restrict__ offsets,
+                                                  const uint8_t *__restrict__ filled, int W, int c, int l0,
+                                                  SegRegion r0, SegRegion r1, uint32_t *__restrict__ Y) {
+  using F = typename C::Fp;
+  constexpr int XW = xyzz_words<F>();
+  constexpr int NCH = XW / 4;  // 16-B chunks per bucket
+  __shared__ uint4 stage[4][NCH][64];
+  static_assert(4 * NCH * 64 * 16 >= 128 * XW * 4, "the fold's park area fits the prefetch image");
+  uint32_t *park = reinterpret_cast<uint32_t *>(&stage[0][0][0]);
+  const int l1 = c - 1 - l0;
+  const int NY = (1 << l0) + (1 << l1);
+  const int nb0 = r0.count * r0.G / 256, nb1 = r1.count * r1.G / 256;  // blocks per window and region
+  const int w = blockIdx.x / (nb0 + nb1);
+  int rb = blockIdx.x % (nb0 + nb1);
+  const bool hiY = rb < nb0;  // Y1 (region 0) or Y0 (region 1)
+  const SegRegion r = hiY ? r0 : r1;
+  if (!hiY) rb -= nb0;
+  const int G = r.G, S = 256 / G;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int seg = rb * S + t % S, part = t / S;
+  const int per = r.len / G;
+  const uint32_t B = 1u << (c - 1);
+  const uint32_t *wb = buckets + (size_t)w * B * XW;
+  auto bucket_m = [&](int s) -> uint32_t {
+    return hiY ? ((uint32_t)seg << l0) + (uint32_t)s : ((uint32_t)s << l0) + (uint32_t)seg;
+  };
+  auto nonempty = [&](uint32_t rank) -> bool {  // empty buckets hold garbage (never written)
+    return filled ? filled[rank] != 0 : offsets[rank + 1] > offsets[rank];
+  };
+  auto prefetch = [&](uint32_t m) {
+    const uint32_t *src = wb + (size_t)m * XW;
+#pragma unroll
+    for (int j = 0; j < NCH; j++)
+      __builtin_amdgcn_global_load_lds((glb_void_t *)(src + 4 * j), (lds_void_t *)&stage[wave][j][0], 16, 0, 0);
+  };
+  auto read_bucket = [&](Xyzz<F> &P) {
+    uint32_t wd[XW];
+#pragma unroll
+    for (int j = 0; j < NCH; j++) {
+      const uint4 v = stage[wave][j][lane];
+      wd[4 * j] = v.x;
+      wd[4 * j + 1] = v.y;
+      wd[4 * j + 2] = v.z;
+      wd[4 * j + 3] = v.w;
+    }
+    xyzz_load(P, wd);
+  };
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  uint32_t m = bucket_m(part * per);
+  bool nfull = nonempty((uint32_t)w * B + m);
+  prefetch(m);
+  for (int k = 0; k < per; k++) {
+    const bool full = nfull;
+    Xyzz<F> cur;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the gather of bucket k has landed in LDS
+    read_bucket(cur);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS image read out before it is refilled
+    if (k + 1 < per) {
+      m = bucket_m(part * per + k + 1);
+      nfull = nonempty((uint32_t)w * B + m);
+      prefetch(m);
+    }
+    if (full) xyzz_add_red(acc, cur);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wavefront is done with its image: the fold reuses the LDS
+  for (int h = 128; h >= S; h >>= 1) {
+    if (t >= h && t < 2 * h) xyzz_store(park + (size_t)(t - h) * XW, acc);
+    __syncthreads();
+    if (t < h) {
+      Xyzz<F> o;
+      xyzz_load(o, park + (size_t)t * XW);
+      xyzz_add_red(acc, o);
+    }
+    __syncthreads();
+  }
+  if (t < S) {
+    const int y = hiY ? (1 << l0) + seg : seg;
+    xyzz_store(Y + ((size_t)w * NY + y) * XW, acc);
+  }
+}
+
 // 7. weighted Y sums by bit jobs: one 256-thread block per (window, job) = 64 quad lanes
 //    (xyzz_add_quad: 4 physical lanes per addition).  Job 0 is the total sum_m B_m, taken
 //    over the 2^l1 sums Y1 (the smaller set); job j in 1..l0 sums the Y0_v with bit j-1 of v
@@ -1233,6 +1328,7 @@ __global__ void __launch_bounds__(256) k_jobsum_blk(const uint32_t *__restrict__
 // The work is nbits n predicated mixed additions -- 8-9x the bucket method's W n -- so the
 // path only pays below a few thousand pairs (msm_bits_max).
 //
+constexpr int BITACC_MAX_K = 256;  // pairs per k_bitacc block (its LDS scalar staging)
 // k_bitacc: block g = pairs [g K, g K + K), thread t = bit t (a wavefront covers 64 bits, so the
 // point of step e is one uniform load for the whole block).  The K scalars are converted to
 // integers (REDC when Montgomery) into LDS first; lane t adds P_e when bit t of k_e is set.
@@ -1243,7 +1339,7 @@ __global__ void __launch_bounds__(256, AccumOcc<typename C::Fp>::waves)
              const uint32_t *__restrict__ points, uint32_t *__restrict__ part) {
   using F = typename C::Fp;
   constexpr int AW = aff_words<F>();
-  __shared__ uint32_t sk[256][9];  // integer scalars of the chunk (8 words, padded)
+  __shared__ uint32_t sk[BITACC_MAX_K][9];  // integer scalars of the chunk (8 words, padded)
   const int t = threadIdx.x, g = blockIdx.x, G = gridDim.x;
   const int p0 = g * K, np = min(K, n - p0);
   for (int e = t; e < np; e += 256) {
@@ -1400,6 +1496,29 @@ static int msm_splits(int n, bool host_inputs, bool one_pass) {
 #ifndef ZK_YSUM_PF
 #define ZK_YSUM_PF 1  // k_ysum2 loads the next bucket one iteration ahead
 #endif
+// Y sums by k_ysum3 (two waves per SIMD, LDS prefetch) when the lanes fill several rounds of one
+// wave per SIMD (ZK_YSUM3_LANES, default 4 x 65536: c = 20 from 2^23 pairs); ZK_YSUM3 = 0 / 1
+// forces k_ysum2 / k_ysum3 (A/B hook, read once)
+inline bool ysum3_on(size_t lanes) {
+  static const int mode = [] {
+    const char *e = getenv("ZK_YSUM3");
+    return e ? atoi(e) : -1;
+  }();
+  static const size_t min_lanes = [] {
+    const char *e = getenv("ZK_YSUM3_LANES");
+    return e ? (size_t)atoll(e) : (size_t)4 * 65536;
+  }();
+  return mode >= 0 ? mode != 0 : lanes >= min_lanes;
+}
+// buckets per Y-sum lane at scale (a power of two; ZK_YSUM_QY overrides it, A/B hook, read once)
+inline int ysum_qy_max() {
+  static const int v = [] {
+    const char *e = getenv("ZK_YSUM_QY");
+    const int q = e ? atoi(e) : 16;
+    return (q >= 1 && q <= 256 && (q & (q - 1)) == 0) ? q : 16;
+  }();
+  return v;
+}
 static MsmShape make_shape(int n, int c, int W, int NS = 1) {
   MsmShape s;
   s.n = n;
@@ -1418,7 +1537,7 @@ static MsmShape make_shape(int n, int c, int W, int NS = 1) {
   {
     const size_t adds = 2 * (size_t)s.W * (size_t)s.B;
     int q = (int)((adds + ZK_YSUM_LANES - 1) / ZK_YSUM_LANES);  // rounded up: at most ZK_YSUM_LANES lanes
-    q = q < 1 ? 1 : (q > 16 ? 16 : q);
+    q = q < 1 ? 1 : (q > ysum_qy_max() ? ysum_qy_max() : q);
     s.QY = pow2(q) < q ? 2 * pow2(q) : pow2(q);  }
   auto clampG = [](int g) { return g < 1 ? 1 : (g > 64 ? 64 : g); };
   s.r0 = SegRegion{1 << s.l1, clampG((1 << s.l0) / s.QY), 1 << s.l0};  // Y1 sums
@@ -1480,7 +1599,7 @@ template <class F>
 constexpr int stitch_bs() { return xyzz_words<F>() > 64 ? 128 : 256; }
 // items per block of the level-0 stitch (the quad-cooperative kernel's 64 for G1)
 template <class F>
-constexpr int stitch_bs0() { return (ZK_STITCH_QUAD && xyzz_words<F>() <= 64) ? STITCH_QBS : stitch_bs<F>(); }
+constexpr int stitch_bs0() { return (ZK_STITCH_QUAD && is_base_field<F>()) ? STITCH_QBS : stitch_bs<F>(); }
 
 static size_t stitch_slots0(const MsmShape &s) {  // item slots of the largest split's accumulation
   size_t m = 0;
@@ -1844,8 +1963,12 @@ struct GroupPass {
     const int n0 = s.r0.count * s.r0.G, n1 = s.r1.count * s.r1.G;
     if (n0 % 256 == 0 && n1 % 256 == 0) {  // block-level Y sums (every shape from c = 12 up)
       const unsigned nblk = (unsigned)(s.W * (n0 + n1) / 256);
-      hipLaunchKernelGGL((k_ysum2<C, ZK_YSUM_PF != 0>), dim3(nblk), dim3(256), 0, st, buckets, offsets,
-                         (const uint8_t *)filled, s.W, c, s.l0, s.r0, s.r1, Y);
+      if (is_base_field<F>() && ysum3_on((size_t)nblk * 256))
+        hipLaunchKernelGGL((k_ysum3<C>), dim3(nblk), dim3(256), 0, st, buckets, offsets, (const uint8_t *)filled, s.W,
+                           c, s.l0, s.r0, s.r1, Y);
+      else
+        hipLaunchKernelGGL((k_ysum2<C, ZK_YSUM_PF != 0>), dim3(nblk), dim3(256), 0, st, buckets, offsets,
+                           (const uint8_t *)filled, s.W, c, s.l0, s.r0, s.r1, Y);
     } else {  // small shapes: in-wavefront segments
       const size_t lanes = (size_t)s.W * s.ylanes;
       hipLaunchKernelGGL(k_ysum<C>, dim3(div_up(lanes, 256)), dim3(256), 0, st, buckets, offsets,
@@ -1980,7 +2103,8 @@ inline int msm_bits_groups(int n) {
     const int v = e ? atoi(e) : 256;
     return v >= 1 ? v : 256;
   }();
-  const int K = (n + g - 1) / g;
+  int K = (n + g - 1) / g;
+  if (K > BITACC_MAX_K) K = BITACC_MAX_K;  // whatever the hooks say: k_bitacc's LDS holds 256 scalars
   return (n + K - 1) / K;
 }
 
@@ -1993,6 +2117,7 @@ static void msm_run_bits(Device &dev, int n, const ScalarSlice &sc_in, const uin
   constexpr int XW = xyzz_words<F>();
   ZK_REQUIRE(nbits >= 1 && nbits <= 256, "msm: bit-job path takes at most 256-bit scalars (internal)");
   const int G = msm_bits_groups(n), K = (n + G - 1) / G;
+  ZK_REQUIRE(K >= 1 && K <= BITACC_MAX_K, "msm: bit-job chunk larger than k_bitacc's LDS staging (internal)");
   hipStream_t st = dev.stream;
   const size_t sc_bytes = host_inputs ? (size_t)n * sc_in.stride * 8 : 0;
   const size_t pt_bytes = host_inputs ? (size_t)n * 2 * C::NP64 * 8 : 0;
@@ -2056,7 +2181,7 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   const bool explicit_window = window >= 4 && window <= 24;
   const int bits = sc_in.mont ? HostOf<C>::Fr::BITS : 64 * sc_in.nread;
   const int c = explicit_window ? window
-                                : (xyzz_words<F>() <= 64 ? msm_default_window_bits(n, bits) : msm_default_window(n));
+                                : (is_base_field<F>() ? msm_default_window_bits(n, bits) : msm_default_window(n));
   // small inputs with the default window: bit jobs, no buckets (an explicit window -- the
   // reference's _variable entry -- always runs the bucket method it names)
   if (!explicit_window && n <= msm_bits_max()) {
@@ -2213,7 +2338,7 @@ size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int windo
   }
   const int c = (window >= 4 && window <= 24)
                     ? window
-                    : (xyzz_words<F>() <= 64 ? msm_default_window_bits(n, nbits) : msm_default_window(n));
+                    : (is_base_field<F>() ? msm_default_window_bits(n, nbits) : msm_default_window(n));
   const int W = nbits / c + 1;
   const int g = groups < 1 ? 1 : (groups > W ? W : groups);
   const int Wg = (W + g - 1) / g;
@@ -2292,15 +2417,10 @@ void msm_g1(int n, const uint64_t *scalars, int nl, const uint64_t *points, bool
     zkh::xyzz_set_inf(acc);
     for (int k = 0; k < G; k++) zkh::xyzz_add(acc, acc, part[k]);
   } else if (G == 1) {  // a one-entry set pins the host-buffer MSM to that device
-    int prev = 0;
-    ZK_CHECK(hipGetDevice(&prev));
-    ZK_CHECK(hipSetDevice(set[0]));
-    {
-      Device &dev = current_device();
-      std::lock_guard<std::mutex> lock(dev.mu);
-      msm_xyzz<C>(dev, n, scalars, nl, points, host_inputs, mont, window, acc);
-    }
-    ZK_CHECK(hipSetDevice(prev));
+    DeviceGuard on(set[0]);
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lock(dev.mu);
+    msm_xyzz<C>(dev, n, scalars, nl, points, host_inputs, mont, window, acc);
   } else {
     Device &dev = current_device();
     std::lock_guard<std::mutex> lock(dev.mu);

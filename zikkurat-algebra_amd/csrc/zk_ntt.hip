@@ -620,12 +620,9 @@ static void enable_peer(int a, int b) {
     (void)hipGetLastError();
     return;
   }
-  int prev = 0;
-  ZK_CHECK(hipGetDevice(&prev));
-  ZK_CHECK(hipSetDevice(a));
+  DeviceGuard on(a);
   const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
   if (e != hipSuccess) (void)hipGetLastError();  // already enabled
-  ZK_CHECK(hipSetDevice(prev));
 }
 
 // chunk k of n bytes (k = 0 .. G-1), 4 KiB aligned boundaries
@@ -837,14 +834,11 @@ void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64
     if (it != set.end()) std::rotate(set.begin(), it, set.end());
   }
   if (set.size() == 1 && set[0] != cur) {  // a one-entry set pins the transform to that device
-    ZK_CHECK(hipSetDevice(set[0]));
-    {
-      Device &dev = current_device();
-      std::lock_guard<std::mutex> lock(dev.mu);
-      if (curve == 0) ntt_run<CfgBN>(dev, curve, m, gen_mont, src, dst, host_io, inverse);
-      else ntt_run<CfgBLS>(dev, curve, m, gen_mont, src, dst, host_io, inverse);
-    }
-    ZK_CHECK(hipSetDevice(cur));
+    DeviceGuard on(set[0]);
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lock(dev.mu);
+    if (curve == 0) ntt_run<CfgBN>(dev, curve, m, gen_mont, src, dst, host_io, inverse);
+    else ntt_run<CfgBLS>(dev, curve, m, gen_mont, src, dst, host_io, inverse);
     return;
   }
   if (set.size() > 1) {
@@ -868,12 +862,9 @@ void ntt(int curve, int m, const uint64_t *gen_mont, const uint64_t *src, uint64
       enable_peer(set[0], set[k]);
       enable_peer(set[k], set[0]);
     }
-    int prev = 0;
-    ZK_CHECK(hipGetDevice(&prev));
-    ZK_CHECK(hipSetDevice(set[0]));
+    DeviceGuard on(set[0]);
     if (curve == 0) ntt_run<CfgBN>(*ctx[0], curve, m, gen_mont, src, dst, host_io, inverse, &sp);
     else ntt_run<CfgBLS>(*ctx[0], curve, m, gen_mont, src, dst, host_io, inverse, &sp);
-    ZK_CHECK(hipSetDevice(prev));
     return;
   }
   Device &dev = current_device();

@@ -124,15 +124,14 @@ Device &device_context(int id, int slot) {
   std::lock_guard<std::mutex> lock(g_devices_mu);
   auto it = g_devices.find({id, slot});
   if (it != g_devices.end()) return *it->second;
-  int prev = 0;
-  ZK_CHECK(hipGetDevice(&prev));
-  if (prev != id) ZK_CHECK(hipSetDevice(id));
+  DeviceGuard on(id);
+  hipStream_t stream = nullptr;
+  ZK_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   Device *d = new Device();
   d->id = id;
   d->slot = slot;
   d->uid = (int)g_devices.size();
-  ZK_CHECK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-  if (prev != id) ZK_CHECK(hipSetDevice(prev));
+  d->stream = stream;
   g_devices[{id, slot}] = d;
   return *d;
 }

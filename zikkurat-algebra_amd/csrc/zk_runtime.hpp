@@ -84,6 +84,24 @@ struct JoinAll {
     if (!(cond)) ::zk::fatal(msg, __FILE__, __LINE__);                    \
   } while (0)
 
+// The calling thread on device `dev` while the guard lives.  The previous device is restored on
+// every exit -- also while a zk::Error unwinds the scope (recoverable error mode) -- and the
+// destructor never throws: a failed restore is cleared from HIP's last-error state instead.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    ZK_CHECK(hipGetDevice(&prev));
+    if (prev != dev) ZK_CHECK(hipSetDevice(dev));
+  }
+  DeviceGuard(const DeviceGuard &) = delete;
+  DeviceGuard &operator=(const DeviceGuard &) = delete;
+  ~DeviceGuard() {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != prev)
+      if (hipSetDevice(prev) != hipSuccess) (void)hipGetLastError();
+  }
+};
+
 // Bump allocator over a grow-only device buffer. reset() at the start of every call.
 // try_reserve() reports an allocation failure (hipMalloc out of memory, or the test hook's
 // cap, arena_set_limit) instead of aborting, so callers can degrade (smaller MSM window

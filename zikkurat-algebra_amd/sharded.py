@@ -63,11 +63,32 @@ def allgather_partials(partial, device=None):
 def rendezvous_path():
     """file through which rank 0 hands the RCCL unique id to the other ranks of one launch.
     The key defaults to (launcher pid, MASTER_PORT): every rank of a torchrun launch is a child
-    of the same agent process, and the port separates concurrent launches.  ZKG_RDZV_KEY /
-    ZKG_RDZV_DIR override it."""
+    of the same agent process, and the port separates concurrent launches.  Launchers whose ranks
+    do not share a parent process (mpirun, srun, a shell loop) must set ZKG_RDZV_KEY to one value
+    per launch on every rank (and ZKG_RDZV_DIR to a directory every rank sees); bench.py's own
+    launcher sets both ZKG_RDZV_KEY and ZKG_RDZV_NONCE."""
     d = os.environ.get("ZKG_RDZV_DIR") or tempfile.gettempdir()
-    key = os.environ.get("ZKG_RDZV_KEY") or f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+    key = os.environ.get("ZKG_RDZV_KEY")
+    if not key:
+        if "TORCHELASTIC_RUN_ID" not in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise RuntimeError("multi-rank run without torchrun: set ZKG_RDZV_KEY (one value per launch, the same "
+                               "on every rank) so the ranks find one rendezvous file")
+        key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
     return os.path.join(d, f"zkg_rdzv_{key}.id")
+
+
+def rendezvous_nonce():
+    """per-launch tag written after the id: a rank accepts only an id file carrying its own
+    launch's tag, so a stale file left by an earlier launch with the same key is never used.
+    ZKG_RDZV_NONCE (bench.py's launcher), else torchrun's run id and restart count; empty (no
+    check) otherwise."""
+    n = os.environ.get("ZKG_RDZV_NONCE")
+    if n:
+        return n.encode()
+    if "TORCHELASTIC_RUN_ID" in os.environ:
+        return (f"{os.environ['TORCHELASTIC_RUN_ID']}:{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}:"
+                f"{os.getppid()}").encode()
+    return b""
 
 
 def _check(rc, what):
@@ -84,32 +105,42 @@ class LibComm:
         self.rank, self.world = rank, world
         uid = ctypes.create_string_buffer(COMM_ID_BYTES)
         path = rendezvous_path()
-        if rank == 0:
-            _check(lib.zkg_comm_unique_id(uid), "zkg_comm_unique_id")
-            tmp = f"{path}.{os.getpid()}.tmp"
-            with open(tmp, "wb") as f:
-                f.write(uid.raw)
-            os.replace(tmp, path)  # atomic: readers see the whole id or nothing
-        else:
-            t0 = time.time()
-            while True:
+        nonce = rendezvous_nonce()
+        try:
+            if rank == 0:
                 try:
-                    with open(path, "rb") as f:
-                        raw = f.read()
-                    if len(raw) == COMM_ID_BYTES:
-                        break
-                except FileNotFoundError:
+                    os.unlink(path)  # a stale id of an earlier launch with this key
+                except OSError:
                     pass
-                if time.time() - t0 > timeout:
-                    raise TimeoutError(f"rank {rank}: no RCCL unique id at {path} after {timeout:.0f} s")
-                time.sleep(0.01)
-            ctypes.memmove(uid, raw, COMM_ID_BYTES)
-        _check(lib.zkg_comm_init(rank, world, uid), "zkg_comm_init")
-        if rank == 0:  # ncclCommInitRank is collective: every rank has read the id by now
-            try:
-                os.unlink(path)
-            except OSError:
-                pass
+                _check(lib.zkg_comm_unique_id(uid), "zkg_comm_unique_id")
+                tmp = f"{path}.{os.getpid()}.tmp"
+                with open(tmp, "wb") as f:
+                    f.write(uid.raw[:COMM_ID_BYTES] + nonce)
+                os.replace(tmp, path)  # atomic: readers see the whole id or nothing
+            else:
+                t0 = time.time()
+                while True:
+                    try:
+                        with open(path, "rb") as f:
+                            raw = f.read()
+                        if len(raw) >= COMM_ID_BYTES and raw[COMM_ID_BYTES:] == nonce:
+                            break
+                    except FileNotFoundError:
+                        pass
+                    if time.time() - t0 > timeout:
+                        raise TimeoutError(f"rank {rank}: no RCCL unique id of this launch at {path} after "
+                                           f"{timeout:.0f} s")
+                    time.sleep(0.01)
+                ctypes.memmove(uid, raw[:COMM_ID_BYTES], COMM_ID_BYTES)
+            _check(lib.zkg_comm_init(rank, world, uid), "zkg_comm_init")
+        finally:
+            # ncclCommInitRank is collective: once rank 0 returns, every rank has read the id (and if
+            # rank 0 failed, its id must not be picked up by anyone later)
+            if rank == 0:
+                try:
+                    os.unlink(path)
+                except OSError:
+                    pass
 
     def barrier(self):
         _check(zk.load().zkg_comm_barrier(), "zkg_comm_barrier")

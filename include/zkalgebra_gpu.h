@@ -314,6 +314,10 @@ ZKG_API void zkg_msm_profile(int on);
 /* test hook: cap on the sorted (window, point) entries one MSM pipeline pass handles
  * (default and maximum 2^30; 0 restores it).  Larger MSMs run in window groups. */
 ZKG_API void zkg_msm_set_group_limit(size_t entries);
+/* test hook: the G1 MSM's Y-sum kernel -- -1: by size (k_ysum3, two waves per SIMD, when the
+ * Y-sum lanes fill several rounds of the chip: c = 20 from 2^23 pairs), 0: always k_ysum2,
+ * 1: always k_ysum3 (block-level shapes, c >= 12) */
+ZKG_API void zkg_msm_set_ysum_mode(int mode);
 /* test hook: NTT pass split -- 12: two passes of 2^9..2^12-point DFTs (4096-element tiles) for
  * every 2^17..2^24; 8: passes of <= 2^8-point DFTs only; 0: the default (two passes at 2^20 only) */
 ZKG_API void zkg_ntt_set_max_radix(int r);

@@ -290,3 +290,22 @@ def test_repeated_points_linearity(gpu, oracle, curve):
     assert np.array_equal(lhs, oracle.msm(curve, ab, pts, mont=True))
     rhs = gpu.msm_affine(curve, np.concatenate([a, b]), np.concatenate([pts, pts]))
     assert np.array_equal(lhs, rhs)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("window,n", [(13, 3000), (16, 20000), (20, 5000)])
+def test_ysum_kernels_vs_oracle(gpu, oracle, curve, mode, window, n):
+    """both G1 Y-sum kernels -- k_ysum2 (one wave per SIMD, register prefetch, quad fold) and
+    k_ysum3 (two waves per SIMD, LDS prefetch, one-lane fold; chosen by size at c = 20 from 2^23)
+    -- forced on the same inputs, mostly-empty buckets included, against the oracle"""
+    sc = oracle.to_std(FR_FLD[curve], gpu.gen_fr(curve, 800 + window, n))
+    pts = gpu.gen_points(curve, 801 + window, n)
+    pts[::97] = np.uint64(0xFFFFFFFFFFFFFFFF)  # infinity inputs
+    want = oracle.normalize(curve, oracle.msm(curve, sc, pts, mont=False, out="proj"))
+    try:
+        gpu.msm_set_ysum_mode(mode)
+        got = gpu.msm_variable(curve, sc, pts, window)
+    finally:
+        gpu.msm_set_ysum_mode(-1)
+    assert np.array_equal(got, want)

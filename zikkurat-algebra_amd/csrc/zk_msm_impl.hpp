@@ -1497,17 +1497,22 @@ static int msm_splits(int n, bool host_inputs, bool one_pass) {
 #define ZK_YSUM_PF 1  // k_ysum2 loads the next bucket one iteration ahead
 #endif
 // Y sums by k_ysum3 (two waves per SIMD, LDS prefetch) when the lanes fill several rounds of one
-// wave per SIMD (ZK_YSUM3_LANES, default 4 x 65536: c = 20 from 2^23 pairs); ZK_YSUM3 = 0 / 1
-// forces k_ysum2 / k_ysum3 (A/B hook, read once)
-inline bool ysum3_on(size_t lanes) {
-  static const int mode = [] {
+// wave per SIMD (ZK_YSUM3_LANES, default 4 x 65536: c = 20 from 2^23 pairs).  Mode -1: that rule,
+// 0 / 1: always k_ysum2 / k_ysum3 (block-level shapes); set by the environment ZK_YSUM3 (A/B hook)
+// or zkg_msm_set_ysum_mode (test hook)
+inline std::atomic<int> &ysum_mode() {
+  static std::atomic<int> v{[] {
     const char *e = getenv("ZK_YSUM3");
-    return e ? atoi(e) : -1;
-  }();
+    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
+  }()};
+  return v;
+}
+inline bool ysum3_on(size_t lanes) {
   static const size_t min_lanes = [] {
     const char *e = getenv("ZK_YSUM3_LANES");
     return e ? (size_t)atoll(e) : (size_t)4 * 65536;
   }();
+  const int mode = ysum_mode().load();
   return mode >= 0 ? mode != 0 : lanes >= min_lanes;
 }
 // buckets per Y-sum lane at scale (a power of two; ZK_YSUM_QY overrides it, A/B hook, read once)

@@ -723,6 +723,8 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   dev.arena.reset();
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
+  HostPrefault prefault;  // the caller's output pages, faulted in while the input copy and the passes run
+  if (host_io && N * elbytes >= ((size_t)16 << 20)) prefault.start(dst, N * elbytes, 8);
   if (host_io) {
     uint64_t *a = dev.arena.take<uint64_t>(N * F::N64);
     d_src = a;
@@ -794,10 +796,10 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     T <<= r;
   }
   if (host_io) {
-    // (A fresh caller array pays its first touch -- ~26 ms per 512 MiB on the MI355X host --
-    // inside this copy; populating the pages from host threads during the passes, or staging
-    // the copy through pinned chunks copied out by 8 threads, measured no gain:
-    // profiles/r03e_split_e2e.txt.)
+    // A fresh caller array would pay its first touch inside this copy (96 vs 18 ms per 512 MiB,
+    // profiles/r03c_*): HostPrefault's 8 threads have populated it meanwhile (round 3 populated
+    // on one thread after the passes, or staged through pinned chunks: no gain, r03e_*).
+    prefault.join();
     if (sp) {
       stream_wait(dev, st);
       spread_out(dev, *sp, dst, d_dst, N * elbytes);

@@ -1,5 +1,6 @@
 // zk_runtime.cpp -- per-device context: stream, grow-only arena, pinned staging.
 #include "zk_runtime.hpp"
+#include <sys/mman.h>
 #include <atomic>
 #include <chrono>
 #include <map>
@@ -281,6 +282,49 @@ void timer_read_all(double *total_ms, long *launches) {
     }
   if (total_ms) *total_ms = t;
   if (launches) *launches = n;
+}
+
+// ---------------------------------------------------------------------------
+// HostPrefault
+
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23  // Linux 5.14
+#endif
+
+static void prefault_range(char *lo, char *hi) {
+  const uintptr_t pg = 4096;
+  char *a = (char *)((uintptr_t)lo & ~(pg - 1));
+  if (madvise(a, (size_t)(hi - a), MADV_POPULATE_WRITE) == 0) return;
+  // no MADV_POPULATE_WRITE: touch every page of the range, writing back the value read
+  for (char *p = lo; p < hi; p = (char *)(((uintptr_t)p + pg) & ~(pg - 1))) {
+    volatile char *v = p;
+    *v = *v;
+  }
+}
+
+bool HostPrefault::enabled() {
+  static const bool on = [] {
+    const char *e = getenv("ZK_PREFAULT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+void HostPrefault::start(void *ptr, size_t bytes, int threads) {
+  join();
+  if (!ptr || !bytes || !enabled()) return;
+  char *base = static_cast<char *>(ptr);
+  const size_t chunk = ((bytes + threads - 1) / threads + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+  for (size_t off = 0; off < bytes; off += chunk) {
+    char *lo = base + off, *hi = base + std::min(bytes, off + chunk);
+    th_.emplace_back([lo, hi] { prefault_range(lo, hi); });
+  }
+}
+
+void HostPrefault::join() {
+  for (auto &t : th_)
+    if (t.joinable()) t.join();
+  th_.clear();
 }
 
 }  // namespace zk

@@ -208,4 +208,26 @@ void timer_read_all(double *total_ms, long *launches);
 
 inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
+// Faults a caller's host OUTPUT range in (writable, contents unchanged) on helper threads while
+// the device works, so the device-to-host copy that ends a host-buffer call lands in resident
+// pages.  A fresh caller array (the Haskell binding allocates one per call, Poly.hs:405) otherwise
+// pays its first touch inside the runtime's pageable copy: 96 ms per 512 MiB against 18 ms into
+// resident pages (profiles/r03c_prefault_and_split_e2e.txt).  MADV_POPULATE_WRITE never changes
+// data, so an output that aliases the input is safe; where the kernel lacks it, each page is read
+// and the same value written back (the copy overwrites the range anyway).  join() (or the
+// destructor) waits for the helpers.
+class HostPrefault {
+ public:
+  HostPrefault() = default;
+  HostPrefault(const HostPrefault &) = delete;
+  HostPrefault &operator=(const HostPrefault &) = delete;
+  void start(void *ptr, size_t bytes, int threads);
+  void join();
+  ~HostPrefault() { join(); }
+  static bool enabled();  // ZK_PREFAULT=0 turns it off (A/B hook, read once)
+
+ private:
+  std::vector<std::thread> th_;
+};
+
 }  // namespace zk

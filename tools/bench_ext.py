@@ -120,54 +120,65 @@ def main():
     dpj.free()
     daf.free()
 
-    # ---------------------------------------------------------------- G1 group FFT
-    fm = 12 if args.quick else 16
-    N = 1 << fm
-    proj = zk.batch_from_affine(CURVE, zk.gen_points(CURVE, 7, N))
-    sg = zk.get_fft_subgroup(CURVE, fm)
-    ds, dd = zk.DeviceBuffer(proj), zk.DeviceBuffer.empty(proj.nbytes)
+    # ---------------------------------------------------------------- G1 group FFT, size sweep
     lib.zkg_g1_fft_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.c_void_p, ctypes.c_void_p]
-    g = sg.gen_array()
     fft = {}
-    for name, inv, smuls in (("forward", 0, N // 2 * fm), ("inverse", 1, N * fm)):
-        sec = timeit(lambda: lib.zkg_g1_fft_device(1, inv, fm, P(g), ds.ptr, dd.ptr), 1)
-        fft[name] = {"log_n": fm, "ms": sec * 1e3, "points_per_s": N / sec, "scalar_muls": smuls,
-                     "scalar_muls_per_s": smuls / sec}
+    sizes = (12, 14) if args.quick else (12, 14, 16, 18, 20)
+    for curve in ("bls12_381", "bn128"):
+        cid = zk.CURVE_ID[curve]
+        for fm in sizes:
+            N = 1 << fm
+            proj = zk.batch_from_affine(curve, zk.gen_points(curve, 7, N))
+            sg = zk.get_fft_subgroup(curve, fm)
+            ds, dd = zk.DeviceBuffer(proj), zk.DeviceBuffer.empty(proj.nbytes)
+            g = sg.gen_array()
+            row = {}
+            for name, inv, smuls in (("forward", 0, N // 2 * fm), ("inverse", 1, N * fm)):
+                sec = timeit(lambda: lib.zkg_g1_fft_device(cid, inv, fm, P(g), ds.ptr, dd.ptr), 1 if fm >= 18 else 3)
+                row[name] = {"ms": sec * 1e3, "points_per_s": N / sec, "scalar_muls": smuls,
+                             "scalar_muls_per_s": smuls / sec, "glv": bool(zk.g1_fft_last_glv())}
+            fft[f"{curve}_2^{fm}"] = row
+            ds.free()
+            dd.free()
     if ref:
         cm = 8
         sg8 = zk.get_fft_subgroup(CURVE, cm)
-        small = proj[:1 << cm].copy()
+        small = zk.batch_from_affine(CURVE, zk.gen_points(CURVE, 7, 1 << cm))
         w = np.zeros_like(small)
         t = cpu_time(lambda: ref.arr(CURVE, "G1_proj_fft_forward", cm, sg8.gen_array(), small, w))
-        fft["forward"]["cpu_reference"] = {"scalar_muls_per_s": (1 << cm) // 2 * cm / t, "cores": 1,
-                                           "sample": "2^8-point forward FFT"}
+        fft["cpu_reference"] = {"scalar_muls_per_s": (1 << cm) // 2 * cm / t, "cores": 1,
+                                "sample": "BLS12-381 2^8-point forward FFT"}
     out["g1_group_fft"] = fft
-    ds.free()
-    dd.free()
 
-    # ---------------------------------------------------------------- G2 MSM
+    # ---------------------------------------------------------------- G2 MSM, both curves
     from test_gpu_g2 import g2_points
-    gm = 16 if args.quick else 18
-    ng = 1 << gm
-    uniq = g2_points(ref, CURVE, min(ng, 1 << 16)) if ref else None
-    if uniq is not None:
-        pts = np.ascontiguousarray(np.resize(uniq, (ng, uniq.shape[1])))
-        sc = zk.gen_fr(CURVE, 8, ng)
-        dsc, dpt = zk.DeviceBuffer(sc), zk.DeviceBuffer(pts)
-        res = np.zeros(36, np.uint64)
-        lib.zkg_g2_msm_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-        sec = timeit(lambda: lib.zkg_g2_msm_device(1, ng, dsc.ptr, 4, 1, dpt.ptr, P(res), 0), 3)
-        g2 = {"n": ng, "ms": sec * 1e3, "pairs_per_s": ng / sec,
-              "roofline": hbm((32 + 192) * ng, sec), "note": "VALU bound (Fp2 products), like G1"}
-        s = 1 << 12
-        w = np.zeros(24, np.uint64)
-        t = cpu_time(lambda: ref.arr(CURVE, "G2_proj_MSM_mont_coeff_affine_out", s, sc[:s], pts[:s], w, 4))
-        g2["cpu_reference"] = {"pairs_per_s": s / t, "cores": 1, "sample": "first 2^12 pairs"}
-        out["g2_msm"] = g2
-        dsc.free()
-        dpt.free()
+    lib.zkg_g2_msm_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    out["g2_msm"] = {}
+    for curve in ("bls12_381", "bn128"):
+        uniq = g2_points(ref, curve, 1 << 14) if ref else None
+        if uniq is None:
+            break
+        for gm in ((16,) if args.quick else (18, 20)):
+            ng = 1 << gm
+            pts = np.ascontiguousarray(np.resize(uniq, (ng, uniq.shape[1])))
+            sc = zk.gen_fr(curve, 8, ng)
+            dsc, dpt = zk.DeviceBuffer(sc), zk.DeviceBuffer(pts)
+            res = np.zeros(36, np.uint64)
+            sec = timeit(lambda: lib.zkg_g2_msm_device(zk.CURVE_ID[curve], ng, dsc.ptr, 4, 1, dpt.ptr, P(res), 0), 3)
+            g2 = {"n": ng, "ms": sec * 1e3, "pairs_per_s": ng / sec,
+                  "roofline": hbm((32 + 4 * 8 * zk.NLIMBS_P[curve]) * ng, sec),
+                  "note": "VALU bound (Fp2 products), like G1; points: 2^14 distinct reference-generated G2 points "
+                          "repeated"}
+            if gm == (16 if args.quick else 18):
+                s_ = 1 << 12
+                w = np.zeros(4 * zk.NLIMBS_P[curve], np.uint64)
+                t = cpu_time(lambda: ref.arr(curve, "G2_proj_MSM_mont_coeff_affine_out", s_, sc[:s_], pts[:s_], w, 4))
+                g2["cpu_reference"] = {"pairs_per_s": s_ / t, "cores": 1, "sample": "first 2^12 pairs"}
+            out["g2_msm"][f"{curve}_2^{gm}"] = g2
+            dsc.free()
+            dpt.free()
     print(json.dumps(out), flush=True)
 
 

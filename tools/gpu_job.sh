@@ -21,6 +21,8 @@
 #   listpmc   rocprofv3 -L (available counters)   -> gpurun_out/TAG_counters.txt
 #   ceiling   tools/microbench/valu_ceiling (prebuilt) -> gpurun_out/TAG_ceiling.json
 #   ext       tools/bench_ext.py                  -> gpurun_out/TAG_ext.json
+#   profext   rocprofv3 --kernel-trace --stats of tools/bench_ext.py -> gpurun_out/TAG_profext/
+#   pmcsqext  rocprofv3 --pmc SQ_* GRBM_GUI_ACTIVE over tools/bench_ext.py --quick (VALU busy per kernel)
 #   phases    MSM phase profile at several sizes  -> gpurun_out/TAG_phases.txt
 #   profsmall rocprofv3 --kernel-trace (per-dispatch timeline) of BLS12-381 2^16 MSMs -> gpurun_out/TAG_profsmall/
 #   cmd       bash tools/job_cmd.sh (scratch commands of the current experiment) -> gpurun_out/TAG_cmd.log
@@ -64,6 +66,11 @@ for step in "$@"; do
     listpmc) timeout -k 10 120 rocprofv3 -L > ${O}_counters.txt 2>&1 ;;
     ceiling) timeout -k 10 120 tools/microbench/valu_ceiling > ${O}_ceiling.json 2> ${O}_ceiling.err ;;
     ext) timeout -k 10 400 python -u tools/bench_ext.py > ${O}_ext.json 2> ${O}_ext.err ;;
+    profext) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d ${O}_profext -o run --output-format csv -- \
+              python3 tools/bench_ext.py > ${O}_profext.json 2> ${O}_profext.err ;;
+    pmcsqext) timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+              GRBM_GUI_ACTIVE -d ${O}_pmcsqext -o run --output-format csv -- python3 tools/bench_ext.py --quick \
+              > /dev/null 2> ${O}_pmcsqext.err ;;
     phases) timeout -k 10 300 python -u tools/sweep_window.py phases > ${O}_phases.txt 2>&1 ;;
     profsmall) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${O}_profsmall -o run --output-format csv -- \
               python3 tools/sweep_window.py bls12_381 16 > ${O}_profsmall.log 2>&1 ;;

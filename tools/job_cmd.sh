@@ -1,24 +1,21 @@
-# r05c: Y sums at large windows -- k_ysum2 (one wave per SIMD) vs k_ysum3 (two waves, LDS
-# prefetch), buckets per lane (QY), window sweep c = 16 / 18 / 20 at 2^23 and 2^24 (the per-GPU
-# config-5 shards at N = 8 / 4), and the 2^23 / 2^26 kernel breakdowns under rocprof
+# r05d: (1) group FFT A/B: round-5 doubling (D = 4XB, shared-reduction Y3, Karatsuba products;
+# in-tree) vs the round-4 point routines (variants/fftold) at 2^12 / 2^16; (2) BLS12-381 MSM at
+# c = 20 from 2^23 with the ballot-counted sub-bin split, vs ZK_SORT_SPLIT=0; kernel breakdown at 2^23
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG}
-for lg in 23 24; do
-  for y in 0 1; do
-    echo "== 2^$lg ZK_YSUM3=$y"
-    ZK_YSUM3=$y timeout -k 10 120 python3 tools/sweep_window.py bls12_381 $lg 16 18 20 || exit 1
-  done
-  for q in 32 64; do
-    echo "== 2^$lg ZK_YSUM3=1 ZK_YSUM_QY=$q"
-    ZK_YSUM3=1 ZK_YSUM_QY=$q timeout -k 10 120 python3 tools/sweep_window.py bls12_381 $lg 20 || exit 1
+for m in 12 16; do
+  for v in new old; do
+    echo "== fft 2^$m $v"
+    if [ $v = old ]; then L=variants/fftold/libzkalgebra_gpu.so; else L=; fi
+    ZK_LIB_PATH=$L timeout -k 10 120 python3 tools/fft_time.py $m 3 || exit 1
   done
 done
-for y in 0 1; do
-  ZK_YSUM3=$y timeout -k 10 200 rocprofv3 --kernel-trace --stats -d ${O}_p23_y$y -o run --output-format csv -- \
-    python3 tools/sweep_window.py bls12_381 23 20 > ${O}_p23_y$y.log 2>&1 || exit 1
+for lg in 23 24 26; do
+  echo "== msm 2^$lg default window"
+  timeout -k 10 200 python3 tools/sweep_window.py bls12_381 $lg 0 || exit 1
 done
-ZK_YSUM3=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${O}_p26_y1 -o run --output-format csv -- \
-  python3 tools/sweep_window.py bls12_381 26 20 > ${O}_p26_y1.log 2>&1 || exit 1
-echo "== 2^26 both"
-for y in 0 1; do ZK_YSUM3=$y timeout -k 10 200 python3 tools/sweep_window.py bls12_381 26 20 || exit 1; done
+echo "== msm 2^23 ZK_SORT_SPLIT=0"
+ZK_SORT_SPLIT=0 timeout -k 10 120 python3 tools/sweep_window.py bls12_381 23 20 || exit 1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d ${O}_p23 -o run --output-format csv -- \
+  python3 tools/sweep_window.py bls12_381 23 20 > ${O}_p23.log 2>&1 || exit 1

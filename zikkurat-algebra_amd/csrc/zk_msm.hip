@@ -27,7 +27,8 @@ int msm_default_window(int n) {
 // The G1 window for `bits`-bit scalars: the table above (swept on BLS12-381's 255-bit Fr), except
 // where a wider window leaves a full top window and measured faster (profiles/r04z_*, r04za_*):
 // BN128 (254 bits = 14 x 17 + 16) takes c = 17 from 2^20 to 2^24 (2^20 2.05 -> 1.97 ms, 2^23
-// 14.0 -> 13.0, 2^24 27.7 -> 26.7), BLS12-381 (255 = 12 x 20 + 15) c = 20 at 2^24 (45.7 -> 41.8 ms).
+// 14.0 -> 13.0, 2^24 27.7 -> 26.7), BLS12-381 (255 = 12 x 20 + 15) c = 20 at 2^24 (45.7 -> 41.8 ms)
+// and, since the two-wave Y sums (k_ysum3), at 2^23 (24.0 -> 23.7 ms; profiles/r05c_*).
 // Windows whose top window holds only the carry (BLS12-381 c = 17 / 19 / 21) put ~n/2 entries in one
 // bucket and lose badly (2^26 c = 21: 302 vs 150 ms).
 int msm_default_window_bits(int n, int bits) {
@@ -35,7 +36,7 @@ int msm_default_window_bits(int n, int bits) {
   if (n <= 1) return c;
   const int lg = ilog2((unsigned)n);
   if (bits == 254 && lg >= 20 && lg <= 24) return 17;
-  if (bits == 255 && lg == 24) return 20;
+  if (bits == 255 && (lg == 23 || lg == 24)) return 20;
   return c;
 }
 

@@ -267,6 +267,34 @@ __global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig
   }
 }
 
+// LDS counter increments for a SMALL key range (nkeys <= 16): one ballot per key value, the
+// lowest lane of each key's group does ONE atomic for the whole group (RET: the others get their
+// slot from the returned base and their rank in the group).  With 8 sub-bins every wavefront
+// instruction of plain atomics hit ~8 lanes per counter: k_split counted 2^23-point inputs at
+// ~5 ps per entry against 1.5 ps with 64 sub-bins (profiles/r05c_ysum_ab_window_sweep.txt).
+template <bool RET>
+__device__ __forceinline__ uint32_t lds_inc_small(uint32_t *ctr, uint32_t key, bool active, int nkeys) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1;
+  uint32_t r = 0;
+  for (int b = 0; b < nkeys; b++) {
+    const bool mine = active && key == (uint32_t)b;
+    const uint64_t m = __ballot(mine);
+    if (m == 0) continue;  // wavefront-uniform
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    if (RET) {
+      uint32_t base = 0;
+      if ((int)lane == leader) base = atomicAdd(&ctr[b], (uint32_t)__popcll(m));
+      base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+      if (mine) r = base + (uint32_t)__popcll(m & below);
+    } else if ((int)lane == leader) {
+      atomicAdd(&ctr[b], (uint32_t)__popcll(m));
+    }
+  }
+  return r;
+}
+constexpr int SPLIT_BALLOT_MAX = 16;  // k_split counts by ballots up to this many sub-bins
+
 // Level 1.5 (large inputs, whose coarse bins outgrow level 2's LDS staging: BLS12-381 2^26 at
 // c = 20 has bins of ~2^18 entries against 8192, and scattering them straight to 2048 fine
 // buckets cost 24 ms of a 165 ms MSM, profiles/r04v_*): every coarse bin q is split by the top
@@ -296,7 +324,15 @@ __global__ void __launch_bounds__(256) k_split(const uint32_t *__restrict__ coff
     if (q == 0 && g == 0 && t == 0) mat[(size_t)gridDim.y * nsub * nwg2] = 0;  // the scan's total slot
     for (int b = t; b < nsub; b += 256) hist[b] = 0;
     __syncthreads();
-    for (uint32_t e = e0 + t; e < e1; e += 256) atomicAdd(&hist[(uint32_t)tmpf[e] >> s2sh], 1u);
+    if (nsub <= SPLIT_BALLOT_MAX) {  // few sub-bins: one atomic per (wavefront, sub-bin)
+      for (uint32_t b0 = e0; b0 < e1; b0 += 256) {  // block-uniform trip count
+        const uint32_t e = b0 + t;
+        const bool act = e < e1;
+        lds_inc_small<false>(hist, act ? (uint32_t)tmpf[e] >> s2sh : 0u, act, nsub);
+      }
+    } else {
+      for (uint32_t e = e0 + t; e < e1; e += 256) atomicAdd(&hist[(uint32_t)tmpf[e] >> s2sh], 1u);
+    }
     __syncthreads();
     for (int b = t; b < nsub; b += 256) cw[(size_t)b * nwg2] = hist[b];
     return;
@@ -314,8 +350,18 @@ __global__ void __launch_bounds__(256) k_split(const uint32_t *__restrict__ coff
       if (e < e1) {
         key[k] = tmpf[e];
         val[k] = tmpv[e];
-        rank[k] = atomicAdd(&hist[key[k] >> s2sh], 1u);
       }
+    }
+    if (nsub <= SPLIT_BALLOT_MAX) {
+#pragma unroll
+      for (int k = 0; k < PER; k++) {
+        const bool act = key[k] != 0xffffffffu;
+        rank[k] = lds_inc_small<true>(hist, act ? key[k] >> s2sh : 0u, act, nsub);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < PER; k++)
+        if (key[k] != 0xffffffffu) rank[k] = atomicAdd(&hist[key[k] >> s2sh], 1u);
     }
     __syncthreads();
     uint32_t tot;
@@ -1968,10 +2014,14 @@ struct GroupPass {
     const int n0 = s.r0.count * s.r0.G, n1 = s.r1.count * s.r1.G;
     if (n0 % 256 == 0 && n1 % 256 == 0) {  // block-level Y sums (every shape from c = 12 up)
       const unsigned nblk = (unsigned)(s.W * (n0 + n1) / 256);
-      if (is_base_field<F>() && ysum3_on((size_t)nblk * 256))
-        hipLaunchKernelGGL((k_ysum3<C>), dim3(nblk), dim3(256), 0, st, buckets, offsets, (const uint8_t *)filled, s.W,
-                           c, s.l0, s.r0, s.r1, Y);
-      else
+      bool two_waves = false;  // k_ysum3 (G1 only: not instantiated for Fp2 points)
+      if constexpr (is_base_field<F>()) {
+        two_waves = ysum3_on((size_t)nblk * 256);
+        if (two_waves)
+          hipLaunchKernelGGL((k_ysum3<C>), dim3(nblk), dim3(256), 0, st, buckets, offsets, (const uint8_t *)filled,
+                             s.W, c, s.l0, s.r0, s.r1, Y);
+      }
+      if (!two_waves)
         hipLaunchKernelGGL((k_ysum2<C, ZK_YSUM_PF != 0>), dim3(nblk), dim3(256), 0, st, buckets, offsets,
                            (const uint8_t *)filled, s.W, c, s.l0, s.r0, s.r1, Y);
     } else {  // small shapes: in-wavefront segments

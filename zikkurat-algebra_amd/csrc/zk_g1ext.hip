@@ -833,12 +833,13 @@ __device__ __forceinline__ void jac_mul_absz(Jac<F> &r, const Jac<F> &p) {
   JacC<F> pc;
   jac_cache(pc, p);
   r = p;
-  for (int b = 62; b >= 0; b--) {
-    jac_dbl(r);
-    if (b == 62 || b == 60 || b == 57 || b == 48 || b == 16) {
-      if (jac_is_inf(p)) continue;
-      jac_add_cached(r, pc);
-    }
+  // runs of doublings between the set bits, each a rolled loop: the fully unrolled chain (63
+  // inlined doublings) held 512 VGPRs and spilled 230 of them to scratch
+  constexpr int kRun[6] = {1, 2, 3, 9, 32, 16};  // doublings before the additions at bits 62, 60, 57, 48, 16; tail
+  for (int s = 0; s < 6; s++) {
+#pragma unroll 1
+    for (int i = 0; i < kRun[s]; i++) jac_dbl(r);
+    if (s < 5 && !jac_is_inf(p)) jac_add_cached(r, pc);
   }
 }
 

@@ -168,6 +168,7 @@ constexpr int MSM_COARSE_BINS = 256;  // coarse bins per window (fewer when B is
 #define ZK_SORT_CHUNK 4096
 #endif
 constexpr int SORT_CHUNK = ZK_SORT_CHUNK;  // level-1 entries staged in LDS at a time (16 per thread)
+constexpr int COUNT_ILP = 8;          // loads in flight per thread in the level-1 / 1.5 counting passes
 constexpr int FINE_LDS_MAX = 8192;    // level-2 bins up to this size are placed in LDS
 constexpr int FINE_LDS_BYTES = 150 * 1024;  // dynamic LDS of k_fine: 2^s counters + staging
 static int fine_stage_cap(int s) {
@@ -213,9 +214,16 @@ __global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig
     if (w == 0 && g == 0 && t == 0) cnt[(size_t)gridDim.y * nbins * nwg] = 0;  // the scan's total slot
     for (int b = t; b < nbins; b += 256) hist[b] = 0;
     __syncthreads();
-    for (int e = e0 + t; e < e1; e += 256) {
-      const uint32_t mag = d[e] & 0x7fffffffu;
-      if (mag) atomicAdd(&hist[(mag - 1) >> s], 1u);
+    for (int b0 = e0; b0 < e1; b0 += 256 * COUNT_ILP) {  // COUNT_ILP digits in flight per thread
+      uint32_t mag[COUNT_ILP];
+#pragma unroll
+      for (int j = 0; j < COUNT_ILP; j++) {
+        const int e = b0 + j * 256 + t;
+        mag[j] = e < e1 ? d[e] & 0x7fffffffu : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < COUNT_ILP; j++)
+        if (mag[j]) atomicAdd(&hist[(mag[j] - 1) >> s], 1u);
     }
     __syncthreads();
     for (int b = t; b < nbins; b += 256) cw[(size_t)b * nwg] = hist[b];
@@ -267,34 +275,6 @@ __global__ void __launch_bounds__(256) k_coarse(const uint32_t *__restrict__ dig
   }
 }
 
-// LDS counter increments for a SMALL key range (nkeys <= 16): one ballot per key value, the
-// lowest lane of each key's group does ONE atomic for the whole group (RET: the others get their
-// slot from the returned base and their rank in the group).  With 8 sub-bins every wavefront
-// instruction of plain atomics hit ~8 lanes per counter: k_split counted 2^23-point inputs at
-// ~5 ps per entry against 1.5 ps with 64 sub-bins (profiles/r05c_ysum_ab_window_sweep.txt).
-template <bool RET>
-__device__ __forceinline__ uint32_t lds_inc_small(uint32_t *ctr, uint32_t key, bool active, int nkeys) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t below = (1ull << lane) - 1;
-  uint32_t r = 0;
-  for (int b = 0; b < nkeys; b++) {
-    const bool mine = active && key == (uint32_t)b;
-    const uint64_t m = __ballot(mine);
-    if (m == 0) continue;  // wavefront-uniform
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    if (RET) {
-      uint32_t base = 0;
-      if ((int)lane == leader) base = atomicAdd(&ctr[b], (uint32_t)__popcll(m));
-      base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-      if (mine) r = base + (uint32_t)__popcll(m & below);
-    } else if ((int)lane == leader) {
-      atomicAdd(&ctr[b], (uint32_t)__popcll(m));
-    }
-  }
-  return r;
-}
-constexpr int SPLIT_BALLOT_MAX = 16;  // k_split counts by ballots up to this many sub-bins
-
 // Level 1.5 (large inputs, whose coarse bins outgrow level 2's LDS staging: BLS12-381 2^26 at
 // c = 20 has bins of ~2^18 entries against 8192, and scattering them straight to 2048 fine
 // buckets cost 24 ms of a 165 ms MSM, profiles/r04v_*): every coarse bin q is split by the top
@@ -324,14 +304,18 @@ __global__ void __launch_bounds__(256) k_split(const uint32_t *__restrict__ coff
     if (q == 0 && g == 0 && t == 0) mat[(size_t)gridDim.y * nsub * nwg2] = 0;  // the scan's total slot
     for (int b = t; b < nsub; b += 256) hist[b] = 0;
     __syncthreads();
-    if (nsub <= SPLIT_BALLOT_MAX) {  // few sub-bins: one atomic per (wavefront, sub-bin)
-      for (uint32_t b0 = e0; b0 < e1; b0 += 256) {  // block-uniform trip count
-        const uint32_t e = b0 + t;
-        const bool act = e < e1;
-        lds_inc_small<false>(hist, act ? (uint32_t)tmpf[e] >> s2sh : 0u, act, nsub);
+    // COUNT_ILP keys in flight per thread before their LDS increments: with one load per
+    // iteration the pass was latency-bound (2 B per lane: 0.58 ms at BLS12-381 2^23, ~0.4 TB/s)
+    for (uint32_t b0 = e0; b0 < e1; b0 += 256 * COUNT_ILP) {
+      uint32_t k[COUNT_ILP];
+#pragma unroll
+      for (int j = 0; j < COUNT_ILP; j++) {
+        const uint32_t e = b0 + j * 256 + t;
+        k[j] = e < e1 ? (uint32_t)tmpf[e] : 0xffffffffu;
       }
-    } else {
-      for (uint32_t e = e0 + t; e < e1; e += 256) atomicAdd(&hist[(uint32_t)tmpf[e] >> s2sh], 1u);
+#pragma unroll
+      for (int j = 0; j < COUNT_ILP; j++)
+        if (k[j] != 0xffffffffu) atomicAdd(&hist[k[j] >> s2sh], 1u);
     }
     __syncthreads();
     for (int b = t; b < nsub; b += 256) cw[(size_t)b * nwg2] = hist[b];
@@ -352,17 +336,9 @@ __global__ void __launch_bounds__(256) k_split(const uint32_t *__restrict__ coff
         val[k] = tmpv[e];
       }
     }
-    if (nsub <= SPLIT_BALLOT_MAX) {
 #pragma unroll
-      for (int k = 0; k < PER; k++) {
-        const bool act = key[k] != 0xffffffffu;
-        rank[k] = lds_inc_small<true>(hist, act ? key[k] >> s2sh : 0u, act, nsub);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < PER; k++)
-        if (key[k] != 0xffffffffu) rank[k] = atomicAdd(&hist[key[k] >> s2sh], 1u);
-    }
+    for (int k = 0; k < PER; k++)
+      if (key[k] != 0xffffffffu) rank[k] = atomicAdd(&hist[key[k] >> s2sh], 1u);
     __syncthreads();
     uint32_t tot;
     const uint32_t h = t < nsub ? hist[t] : 0u;

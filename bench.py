@@ -758,8 +758,12 @@ def end_to_end(zk, curve, scalars, points, device_ms, ntt, args, device_aff, rep
                          "ms_reused_output": dt2 * 1e3, "elems_per_s_reused_output": x.shape[0] / dt2,
                          "device_resident_ms": dev, "pcie_bytes": 2 * x.nbytes,
                          "pcie_GBps_effective": 2 * x.nbytes / max(dt2 - dev * 1e-3, 1e-9) / 1e9,
-                         "note": "ms: fresh numpy output per call (its first touch -- 512 MiB of new pages -- is "
-                                 "paid inside the call); ms_reused_output: the same symbol into a resident buffer"}
+                         "note": "ms: a fresh, uninitialised output array per call (np.empty, as the binding's "
+                                 "mallocForeignPtrArray, Poly.hs:405): its first touch -- 512 MiB of new pages -- "
+                                 "is paid inside the call, where the library's helper threads prefault it during "
+                                 "the input copy and the passes; ms_reused_output: the same symbol into a resident "
+                                 "buffer.  (Round 4 allocated with np.zeros inside the timing: +~25 ms of calloc "
+                                 "zeroing that the Haskell binding never pays.)"}
     return out
 
 

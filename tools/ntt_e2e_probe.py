@@ -80,6 +80,17 @@ def main():
     tp, _ = populate(b, 8)
     print(f"ntt_forward populated first ({tp:.1f} ms populate): "
           f"{ms(lambda: sym(m, zk._p(g), zk._p(x), zk._p(b))):7.2f} ms", flush=True)
+    for name, alloc in (("np.zeros_like", np.zeros_like), ("np.empty_like", np.empty_like)):
+        for _ in range(2):
+            t = time.perf_counter()
+            b = alloc(x)
+            ta = (time.perf_counter() - t) * 1e3
+            keep.append(b)
+            tc = ms(lambda: sym(m, zk._p(g), zk._p(x), zk._p(b)))
+            print(f"{name}: alloc {ta:7.2f} ms, then ntt_forward into it {tc:7.2f} ms", flush=True)
+    for _ in range(2):
+        print(f"zk.forward_ntt (wrapper, empty output): {ms(lambda: keep.append(zk.forward_ntt(sg, x))):7.2f} ms",
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -859,11 +859,19 @@ __global__ void __launch_bounds__(256) k_subgroup_check(int n, const uint32_t *_
     xyzz_load(v, A + i * xw<F>());
     if (xyzz_is_inf(v)) continue;
     Jac<F> p, r;
-    xyzz_to_jac(p, v);
-    {  // [lambda] P = [|z|]([|z|] P) - P (lambda = z^2 - 1; |z| = 0xd201000000010000 has 6 bits set)
-      Jac<F> zp;
-      jac_mul_absz(zp, p);
-      jac_mul_absz(r, zp);
+    {  // [lambda] P = [|z|]([|z|] P) - P (lambda = z^2 - 1; |z| = 0xd201000000010000 has 6 bits set).
+      // The two [|z|] chains run as ONE rolled loop body and P is re-read from A afterwards
+      // instead of staying live across them: kept live and inlined twice, the kernel held 512
+      // VGPRs and spilled ~260 to scratch inside the doubling chains.
+      xyzz_to_jac(r, v);
+#pragma unroll 1
+      for (int rep = 0; rep < 2; rep++) {
+        Jac<F> t;
+        jac_mul_absz(t, r);
+        r = t;
+      }
+      xyzz_load(v, A + i * xw<F>());
+      xyzz_to_jac(p, v);
       Jac<F> np = p;
       fe_neg(np.Y, p.Y);
       JacC<F> nc;

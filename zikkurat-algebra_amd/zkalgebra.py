@@ -307,7 +307,7 @@ def forward_ntt(sg, poly):
     if poly.ndim != 2 or sg.size != poly.shape[0]:
         raise ValueError("forwardNTT: subgroup size differs from the array size")   # Poly.hs:403
     require_gpu()
-    out = np.zeros_like(poly)
+    out = np.empty_like(poly)  # every element is written (as the binding's mallocForeignPtrArray)
     getattr(load(), f"{sg.curve}_poly_mont_ntt_forward")(sg.log_size, _p(sg.gen_array()), _p(poly), _p(out))
     return out
 
@@ -317,7 +317,7 @@ def inverse_ntt(sg, values):
     if values.ndim != 2 or sg.size != values.shape[0]:
         raise ValueError("inverseNTT: subgroup size differs from the array size")   # Poly.hs:415
     require_gpu()
-    out = np.zeros_like(values)
+    out = np.empty_like(values)  # every element is written
     getattr(load(), f"{sg.curve}_poly_mont_ntt_inverse")(sg.log_size, _p(sg.gen_array()), _p(values), _p(out))
     return out
 

@@ -50,11 +50,27 @@ def main():
     zk.require_gpu()
     x = zk.gen_fr("bls12_381", 0x5A4B0003, n)
     print(f"prefault {'off' if os.environ.get('ZK_PREFAULT') == '0' else 'on'}, 2^{m} x 32 B = {x.nbytes >> 20} MiB", flush=True)
-    for th in (1, 8, 16):
-        b = np.zeros_like(x)
-        t, rcs = populate(b, th)
-        print(f"populate {th:2d} threads: {t:7.2f} ms (rc {set(rcs)})", flush=True)
-        del b
+    hold = []
+    for alloc in ("zeros", "empty"):
+        for th in (1, 8, 16):
+            b = np.zeros_like(x) if alloc == "zeros" else np.empty_like(x)
+            t, rcs = populate(b, th)
+            print(f"populate ({alloc:5s} buffer) {th:2d} threads: {t:7.2f} ms (rc {set(rcs)})", flush=True)
+            hold.append(b)  # kept: a freed mapping could come back populated
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    for _ in range(2):
+        b = np.empty_like(x)
+        t = time.perf_counter()
+        rc = hip.hipHostRegister(b.ctypes.data, b.nbytes, 0)
+        tr = (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
+        rc2 = hip.hipHostUnregister(b.ctypes.data)
+        tu = (time.perf_counter() - t) * 1e3
+        print(f"hipHostRegister fresh empty buffer: {tr:7.2f} ms (rc {rc}), unregister {tu:6.2f} ms (rc {rc2})", flush=True)
+        hold.append(b)
+    del hold
     d = zk.DeviceBuffer(x)
     res = np.zeros_like(x)
     res.fill(1)

@@ -723,8 +723,8 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   dev.arena.reset();
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
-  HostPrefault prefault;  // the caller's output pages, faulted in while the input copy and the passes run
-  if (host_io && N * elbytes >= ((size_t)16 << 20)) prefault.start(dst, N * elbytes, 8);
+  HostPrefault prefault;  // the caller's output pages (started after the input copy, below)
+  constexpr size_t OUT_PIECE = (size_t)32 << 20;
   if (host_io) {
     uint64_t *a = dev.arena.take<uint64_t>(N * F::N64);
     d_src = a;
@@ -745,6 +745,9 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     } else {
       ZK_CHECK(hipMemcpyAsync(a, src, N * elbytes, hipMemcpyHostToDevice, st));
     }
+    // the pageable copy above has read the caller's input by now: populate the output's pages
+    // while the passes run and the copy back proceeds piece by piece
+    if (N * elbytes >= 2 * OUT_PIECE) prefault.start(dst, N * elbytes, OUT_PIECE, 8);
   }
   uint64_t *scratch = dev.arena.take<uint64_t>(N * F::N64);
 
@@ -796,15 +799,19 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     T <<= r;
   }
   if (host_io) {
-    // A fresh caller array would pay its first touch inside this copy (96 vs 18 ms per 512 MiB,
-    // profiles/r03c_*): HostPrefault's 8 threads have populated it meanwhile (round 3 populated
-    // on one thread after the passes, or staged through pinned chunks: no gain, r03e_*).
-    prefault.join();
+    // A fresh caller array would pay its first touch inside this copy: the copy follows
+    // HostPrefault piece by piece (piece k leaves once its pages are resident)
     if (sp) {
+      prefault.join();
       stream_wait(dev, st);
       spread_out(dev, *sp, dst, d_dst, N * elbytes);
     } else {
-      ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
+      const size_t bytes = N * elbytes;
+      for (size_t off = 0, k = 0; off < bytes; off += OUT_PIECE, k++) {
+        prefault.wait_piece(k);
+        ZK_CHECK(hipMemcpyAsync((char *)dst + off, (const char *)d_dst + off, std::min(OUT_PIECE, bytes - off),
+                                hipMemcpyDeviceToHost, st));
+      }
     }
   }
   stream_wait(dev, st);

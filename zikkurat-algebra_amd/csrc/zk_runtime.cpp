@@ -310,21 +310,35 @@ bool HostPrefault::enabled() {
   return on;
 }
 
-void HostPrefault::start(void *ptr, size_t bytes, int threads) {
+void HostPrefault::start(void *ptr, size_t bytes, size_t piece, int threads) {
   join();
-  if (!ptr || !bytes || !enabled()) return;
+  if (!ptr || !bytes || !piece || !enabled()) return;
   char *base = static_cast<char *>(ptr);
-  const size_t chunk = ((bytes + threads - 1) / threads + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
-  for (size_t off = 0; off < bytes; off += chunk) {
-    char *lo = base + off, *hi = base + std::min(bytes, off + chunk);
-    th_.emplace_back([lo, hi] { prefault_range(lo, hi); });
-  }
+  npieces_ = (bytes + piece - 1) / piece;
+  done_.reset(new std::atomic<int>[npieces_]);
+  for (size_t k = 0; k < npieces_; k++) done_[k].store(0, std::memory_order_relaxed);
+  next_.store(0);
+  for (int t = 0; t < threads && (size_t)t < npieces_; t++)
+    th_.emplace_back([this, base, bytes, piece] {
+      for (;;) {
+        const size_t k = next_.fetch_add(1);
+        if (k >= npieces_) return;
+        prefault_range(base + k * piece, base + std::min(bytes, (k + 1) * piece));
+        done_[k].store(1, std::memory_order_release);
+      }
+    });
+}
+
+void HostPrefault::wait_piece(size_t k) {
+  if (th_.empty() || k >= npieces_) return;
+  while (!done_[k].load(std::memory_order_acquire)) std::this_thread::yield();
 }
 
 void HostPrefault::join() {
   for (auto &t : th_)
     if (t.joinable()) t.join();
   th_.clear();
+  npieces_ = 0;
 }
 
 }  // namespace zk

@@ -10,7 +10,9 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <atomic>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -208,26 +210,32 @@ void timer_read_all(double *total_ms, long *launches);
 
 inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
-// Faults a caller's host OUTPUT range in (writable, contents unchanged) on helper threads while
-// the device works, so the device-to-host copy that ends a host-buffer call lands in resident
-// pages.  A fresh caller array (the Haskell binding allocates one per call, Poly.hs:405) otherwise
-// pays its first touch inside the runtime's pageable copy: 96 ms per 512 MiB against 18 ms into
-// resident pages (profiles/r03c_prefault_and_split_e2e.txt).  MADV_POPULATE_WRITE never changes
-// data, so an output that aliases the input is safe; where the kernel lacks it, each page is read
-// and the same value written back (the copy overwrites the range anyway).  join() (or the
-// destructor) waits for the helpers.
+// Faults a caller's host OUTPUT range in (writable, contents unchanged) on helper threads, piece
+// by piece in increasing order, so the device-to-host copy that ends a host-buffer call lands in
+// resident pages: the caller copies piece k as soon as wait_piece(k) returns while the helpers
+// populate the later pieces.  A fresh caller array (the Haskell binding allocates one per call,
+// Poly.hs:405) otherwise pays its first touch inside the runtime's pageable copy: a 2^24 NTT
+// into a fresh array took 35 ms against 22 ms into resident pages (profiles/r05g_*).  Populating
+// 512 MiB takes ~19 ms on one thread and ~9 ms on 8 (page zeroing); beside the pageable input
+// copy it slowed that copy down, so it starts after it.  MADV_POPULATE_WRITE never changes data,
+// so an output that aliases the input is safe; where the kernel lacks it, each page is read and
+// the same value written back.
 class HostPrefault {
  public:
   HostPrefault() = default;
   HostPrefault(const HostPrefault &) = delete;
   HostPrefault &operator=(const HostPrefault &) = delete;
-  void start(void *ptr, size_t bytes, int threads);
+  void start(void *ptr, size_t bytes, size_t piece, int threads);
+  void wait_piece(size_t k);  // piece k is resident (at once when disabled or not started)
   void join();
   ~HostPrefault() { join(); }
   static bool enabled();  // ZK_PREFAULT=0 turns it off (A/B hook, read once)
 
  private:
   std::vector<std::thread> th_;
+  std::unique_ptr<std::atomic<int>[]> done_;
+  std::atomic<size_t> next_{0};
+  size_t npieces_ = 0;
 };
 
 }  // namespace zk

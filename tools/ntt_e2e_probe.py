@@ -20,9 +20,12 @@ libc = ctypes.CDLL("libc.so.6", use_errno=True)
 libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
 
 
-def populate(buf, threads):
+def populate(buf, threads, huge=False):
     addr, nbytes = buf.ctypes.data, buf.nbytes
     page = 4096
+    if huge:  # transparent huge pages for the whole range first
+        a = addr & ~(page - 1)
+        libc.madvise(a, addr + nbytes - a, 14)  # MADV_HUGEPAGE
     chunk = (nbytes // threads + (2 << 20) - 1) & ~((2 << 20) - 1)
     rcs = []
 
@@ -57,6 +60,16 @@ def main():
             t, rcs = populate(b, th)
             print(f"populate ({alloc:5s} buffer) {th:2d} threads: {t:7.2f} ms (rc {set(rcs)})", flush=True)
             hold.append(b)  # kept: a freed mapping could come back populated
+    try:
+        print("THP:", open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip(),
+              "defrag:", open("/sys/kernel/mm/transparent_hugepage/defrag").read().strip(), flush=True)
+    except OSError as e:
+        print("THP settings unreadable:", e)
+    for th in (1, 8, 16):
+        b = np.empty_like(x)
+        t, rcs = populate(b, th, huge=True)
+        print(f"populate (empty buffer, MADV_HUGEPAGE) {th:2d} threads: {t:7.2f} ms (rc {set(rcs)})", flush=True)
+        hold.append(b)
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
     hip.hipHostUnregister.argtypes = [ctypes.c_void_p]

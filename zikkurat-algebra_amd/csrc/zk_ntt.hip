@@ -724,7 +724,6 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
   HostPrefault prefault;  // the caller's output pages (started after the input copy, below)
-  constexpr size_t OUT_PIECE = (size_t)32 << 20;
   if (host_io) {
     uint64_t *a = dev.arena.take<uint64_t>(N * F::N64);
     d_src = a;
@@ -746,8 +745,8 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
       ZK_CHECK(hipMemcpyAsync(a, src, N * elbytes, hipMemcpyHostToDevice, st));
     }
     // the pageable copy above has read the caller's input by now: populate the output's pages
-    // while the passes run and the copy back proceeds piece by piece
-    if (N * elbytes >= 2 * OUT_PIECE) prefault.start(dst, N * elbytes, OUT_PIECE, 8);
+    // while the passes run
+    if (N * elbytes >= ((size_t)16 << 20)) prefault.start(dst, N * elbytes, 8);
   }
   uint64_t *scratch = dev.arena.take<uint64_t>(N * F::N64);
 
@@ -799,19 +798,14 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     T <<= r;
   }
   if (host_io) {
-    // A fresh caller array would pay its first touch inside this copy: the copy follows
-    // HostPrefault piece by piece (piece k leaves once its pages are resident)
+    // a fresh caller array would pay its first touch inside this copy: HostPrefault has
+    // populated it while the passes ran
+    prefault.join();
     if (sp) {
-      prefault.join();
       stream_wait(dev, st);
       spread_out(dev, *sp, dst, d_dst, N * elbytes);
     } else {
-      const size_t bytes = N * elbytes;
-      for (size_t off = 0, k = 0; off < bytes; off += OUT_PIECE, k++) {
-        prefault.wait_piece(k);
-        ZK_CHECK(hipMemcpyAsync((char *)dst + off, (const char *)d_dst + off, std::min(OUT_PIECE, bytes - off),
-                                hipMemcpyDeviceToHost, st));
-      }
+      ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
     }
   }
   stream_wait(dev, st);

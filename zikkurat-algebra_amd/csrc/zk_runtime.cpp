@@ -310,35 +310,25 @@ bool HostPrefault::enabled() {
   return on;
 }
 
-void HostPrefault::start(void *ptr, size_t bytes, size_t piece, int threads) {
+void HostPrefault::start(void *ptr, size_t bytes, int threads) {
   join();
-  if (!ptr || !bytes || !piece || !enabled()) return;
+  if (!ptr || !bytes || threads < 1 || !enabled()) return;
   char *base = static_cast<char *>(ptr);
-  npieces_ = (bytes + piece - 1) / piece;
-  done_.reset(new std::atomic<int>[npieces_]);
-  for (size_t k = 0; k < npieces_; k++) done_[k].store(0, std::memory_order_relaxed);
-  next_.store(0);
-  for (int t = 0; t < threads && (size_t)t < npieces_; t++)
-    th_.emplace_back([this, base, bytes, piece] {
-      for (;;) {
-        const size_t k = next_.fetch_add(1);
-        if (k >= npieces_) return;
-        prefault_range(base + k * piece, base + std::min(bytes, (k + 1) * piece));
-        done_[k].store(1, std::memory_order_release);
-      }
-    });
-}
-
-void HostPrefault::wait_piece(size_t k) {
-  if (th_.empty() || k >= npieces_) return;
-  while (!done_[k].load(std::memory_order_acquire)) std::this_thread::yield();
+  // transparent huge pages for the 2 MiB-aligned interior (a hint: fewer, larger page faults)
+  const uintptr_t huge = (uintptr_t)2 << 20;
+  const uintptr_t h0 = ((uintptr_t)base + huge - 1) & ~(huge - 1), h1 = ((uintptr_t)base + bytes) & ~(huge - 1);
+  if (h1 > h0) (void)madvise((void *)h0, h1 - h0, MADV_HUGEPAGE);
+  const size_t piece = ((bytes + threads - 1) / threads + huge - 1) & ~(size_t)(huge - 1);
+  for (size_t off = 0; off < bytes; off += piece) {
+    char *lo = base + off, *hi = base + std::min(bytes, off + piece);
+    th_.emplace_back([lo, hi] { prefault_range(lo, hi); });
+  }
 }
 
 void HostPrefault::join() {
   for (auto &t : th_)
     if (t.joinable()) t.join();
   th_.clear();
-  npieces_ = 0;
 }
 
 }  // namespace zk

@@ -210,14 +210,15 @@ void timer_read_all(double *total_ms, long *launches);
 
 inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
-// Faults a caller's host OUTPUT range in (writable, contents unchanged) on helper threads, piece
-// by piece in increasing order, so the device-to-host copy that ends a host-buffer call lands in
-// resident pages: the caller copies piece k as soon as wait_piece(k) returns while the helpers
-// populate the later pieces.  A fresh caller array (the Haskell binding allocates one per call,
-// Poly.hs:405) otherwise pays its first touch inside the runtime's pageable copy: a 2^24 NTT
-// into a fresh array took 35 ms against 22 ms into resident pages (profiles/r05g_*).  Populating
-// 512 MiB takes ~19 ms on one thread and ~9 ms on 8 (page zeroing); beside the pageable input
-// copy it slowed that copy down, so it starts after it.  MADV_POPULATE_WRITE never changes data,
+// Faults a caller's host OUTPUT range in (writable, contents unchanged) on helper threads while
+// the device works, so the device-to-host copy that ends a host-buffer call lands in resident
+// pages.  A fresh caller array (the Haskell binding allocates one per call, Poly.hs:405) otherwise
+// pays its first touch inside the runtime's pageable copy: a 2^24 NTT into a fresh array took
+// 35-43 ms against 22 ms into resident pages (profiles/r05g_*, r05h_*).  Populating 512 MiB takes
+// ~19 ms on one thread and 6-9 ms on 8 (page zeroing; transparent huge pages requested for the
+// range first: 6.2 vs 7.3 ms, r05i_*); beside the pageable input copy it slowed that copy down,
+// and copying back piece by piece behind it cost ~2.5 ms in copy calls, so the callers start it
+// after the input copy and join it before one copy back.  MADV_POPULATE_WRITE never changes data,
 // so an output that aliases the input is safe; where the kernel lacks it, each page is read and
 // the same value written back.
 class HostPrefault {
@@ -225,17 +226,13 @@ class HostPrefault {
   HostPrefault() = default;
   HostPrefault(const HostPrefault &) = delete;
   HostPrefault &operator=(const HostPrefault &) = delete;
-  void start(void *ptr, size_t bytes, size_t piece, int threads);
-  void wait_piece(size_t k);  // piece k is resident (at once when disabled or not started)
+  void start(void *ptr, size_t bytes, int threads);
   void join();
   ~HostPrefault() { join(); }
   static bool enabled();  // ZK_PREFAULT=0 turns it off (A/B hook, read once)
 
  private:
   std::vector<std::thread> th_;
-  std::unique_ptr<std::atomic<int>[]> done_;
-  std::atomic<size_t> next_{0};
-  size_t npieces_ = 0;
 };
 
 }  // namespace zk

@@ -723,7 +723,7 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   dev.arena.reset();
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
-  HostPrefault prefault;  // the caller's output pages (started after the input copy, below)
+  HostPrefault prefault;  // the caller's output pages (started once the passes are enqueued, below)
   if (host_io) {
     uint64_t *a = dev.arena.take<uint64_t>(N * F::N64);
     d_src = a;
@@ -744,9 +744,6 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     } else {
       ZK_CHECK(hipMemcpyAsync(a, src, N * elbytes, hipMemcpyHostToDevice, st));
     }
-    // the pageable copy above has read the caller's input by now: populate the output's pages
-    // while the passes run
-    if (N * elbytes >= ((size_t)16 << 20)) prefault.start(dst, N * elbytes, 8);
   }
   uint64_t *scratch = dev.arena.take<uint64_t>(N * F::N64);
 
@@ -798,8 +795,11 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     T <<= r;
   }
   if (host_io) {
-    // a fresh caller array would pay its first touch inside this copy: HostPrefault has
-    // populated it while the passes ran
+    // A fresh caller array would pay its first touch inside the copy back: populate its pages
+    // now, while the passes run.  Started only after the passes are enqueued: MADV_POPULATE_WRITE
+    // holds the address-space lock shared, so a runtime mapping made during a launch waited for
+    // the whole populate (a 10 ms gap before the first pass, profiles/r05k_*).
+    if (N * elbytes >= ((size_t)16 << 20)) prefault.start(dst, N * elbytes, 8);
     prefault.join();
     if (sp) {
       stream_wait(dev, st);

@@ -216,9 +216,10 @@ inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b);
 // pays its first touch inside the runtime's pageable copy: a 2^24 NTT into a fresh array took
 // 35-43 ms against 22 ms into resident pages (profiles/r05g_*, r05h_*).  Populating 512 MiB takes
 // ~19 ms on one thread and 6-9 ms on 8 (page zeroing; transparent huge pages requested for the
-// range first: 6.2 vs 7.3 ms, r05i_*); beside the pageable input copy it slowed that copy down,
-// and copying back piece by piece behind it cost ~2.5 ms in copy calls, so the callers start it
-// after the input copy and join it before one copy back.  MADV_POPULATE_WRITE never changes data,
+// range first: 6.2 vs 7.3 ms, r05i_*).  Beside the pageable input copy it slowed that copy
+// down, copying back piece by piece behind it cost ~2.5 ms in copy calls, and started before a
+// kernel launch it delayed the launch (the populate holds the address-space lock shared), so the
+// NTT starts it once its passes are enqueued and joins it before one copy back.  MADV_POPULATE_WRITE never changes data,
 // so an output that aliases the input is safe; where the kernel lacks it, each page is read and
 // the same value written back.
 class HostPrefault {

@@ -1,4 +1,4 @@
-# r05l: host-buffer NTT into fresh outputs with the prefault started after the pass launches
+# r05n: host-buffer NTT copy-back through pinned pieces + 8 host threads (fresh vs resident outputs)
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/${TAG}

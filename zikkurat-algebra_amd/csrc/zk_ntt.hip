@@ -723,7 +723,6 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
   dev.arena.reset();
   const uint64_t *d_src = src;
   uint64_t *d_dst = dst;
-  HostPrefault prefault;  // the caller's output pages (started once the passes are enqueued, below)
   if (host_io) {
     uint64_t *a = dev.arena.take<uint64_t>(N * F::N64);
     d_src = a;
@@ -795,17 +794,11 @@ static void ntt_run(Device &dev, int curve, int m, const uint64_t *gen_mont, con
     T <<= r;
   }
   if (host_io) {
-    // A fresh caller array would pay its first touch inside the copy back: populate its pages
-    // now, while the passes run.  Started only after the passes are enqueued: MADV_POPULATE_WRITE
-    // holds the address-space lock shared, so a runtime mapping made during a launch waited for
-    // the whole populate (a 10 ms gap before the first pass, profiles/r05k_*).
-    if (N * elbytes >= ((size_t)16 << 20)) prefault.start(dst, N * elbytes, 8);
-    prefault.join();
     if (sp) {
       stream_wait(dev, st);
       spread_out(dev, *sp, dst, d_dst, N * elbytes);
     } else {
-      ZK_CHECK(hipMemcpyAsync(dst, d_dst, N * elbytes, hipMemcpyDeviceToHost, st));
+      copy_to_host(dev, st, dst, d_dst, N * elbytes);  // pinned pieces + 8 host threads (zk_runtime.hpp)
     }
   }
   stream_wait(dev, st);

@@ -164,6 +164,10 @@ struct Device {
   void *pinned = nullptr;
   size_t pinned_cap = 0;
   void *host_staging(size_t bytes);
+  // pinned double buffer of the large device-to-host copies into caller memory (copy_to_host)
+  void *xfer = nullptr;
+  size_t xfer_cap = 0;
+  hipEvent_t xfer_ev[2] = {nullptr, nullptr};
   KernelTimer timer;
   hipEvent_t sync_ev = nullptr;  // stream_wait's marker
   // second stream of this context (host-input copies overlapping the first stream's work) and
@@ -179,6 +183,16 @@ struct Device {
   hipEvent_t split_event(int h);
   void release_memory();         // arena + pinned staging (caller holds mu, stream idle)
 };
+
+// Copy `bytes` from device memory `src` (ordered after the work on `st`) into CALLER host memory
+// `dst` and wait (caller holds dev.mu).  Large copies go through the context's pinned double
+// buffer in 32 MiB pieces: the DMA engine fills one half while the host pool copies the other
+// into `dst` on 8 threads.  A caller's output array is often FRESH (the Haskell binding allocates
+// one per call, Poly.hs:405): through the runtime's pageable path the first touch of its pages
+// cost a 2^24 NTT 35-43 ms against 22 ms into resident pages -- the runtime pins the destination
+// in place (fault + pin inside the call) and unpins it later -- while 8 host threads fault the
+// pages in as they copy (profiles/r05g_*..r05n_*).  Small copies take the plain pageable path.
+void copy_to_host(Device &dev, hipStream_t st, void *dst, const void *src, size_t bytes);
 
 // Wait for everything enqueued on st by spinning on an event (caller holds dev.mu): the
 // synchronous entry points return as soon as the GPU is done, without the wake-up latency of
@@ -209,31 +223,5 @@ void timer_reset_all();
 void timer_read_all(double *total_ms, long *launches);
 
 inline unsigned div_up(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
-
-// Faults a caller's host OUTPUT range in (writable, contents unchanged) on helper threads while
-// the device works, so the device-to-host copy that ends a host-buffer call lands in resident
-// pages.  A fresh caller array (the Haskell binding allocates one per call, Poly.hs:405) otherwise
-// pays its first touch inside the runtime's pageable copy: a 2^24 NTT into a fresh array took
-// 35-43 ms against 22 ms into resident pages (profiles/r05g_*, r05h_*).  Populating 512 MiB takes
-// ~19 ms on one thread and 6-9 ms on 8 (page zeroing; transparent huge pages requested for the
-// range first: 6.2 vs 7.3 ms, r05i_*).  Beside the pageable input copy it slowed that copy
-// down, copying back piece by piece behind it cost ~2.5 ms in copy calls, and started before a
-// kernel launch it delayed the launch (the populate holds the address-space lock shared), so the
-// NTT starts it once its passes are enqueued and joins it before one copy back.  MADV_POPULATE_WRITE never changes data,
-// so an output that aliases the input is safe; where the kernel lacks it, each page is read and
-// the same value written back.
-class HostPrefault {
- public:
-  HostPrefault() = default;
-  HostPrefault(const HostPrefault &) = delete;
-  HostPrefault &operator=(const HostPrefault &) = delete;
-  void start(void *ptr, size_t bytes, int threads);
-  void join();
-  ~HostPrefault() { join(); }
-  static bool enabled();  // ZK_PREFAULT=0 turns it off (A/B hook, read once)
-
- private:
-  std::vector<std::thread> th_;
-};
 
 }  // namespace zk

@@ -418,8 +418,8 @@ struct Stage {
     return d;
   }
   uint64_t *out(uint64_t *p, size_t n) { return host ? dev.arena.take<uint64_t>(n * 4) : p; }
-  void back(uint64_t *host_p, const uint64_t *dev_p, size_t n) {
-    if (host && n) ZK_CHECK(hipMemcpyAsync(host_p, dev_p, n * 32, hipMemcpyDeviceToHost, dev.stream));
+  void back(uint64_t *host_p, const uint64_t *dev_p, size_t n) {  // waits (pinned pieces for large outputs)
+    if (host && n) copy_to_host(dev, dev.stream, host_p, dev_p, n * 32);
   }
 };
 

@@ -1021,7 +1021,7 @@ static void batch_from_affine_t(Device &dev, int n, const uint64_t *src, uint64_
   }
   hipLaunchKernelGGL(k_from_affine<C>, dim3(div_up(N, 256)), dim3(256), 0, st, n, ds, dt, one_ref<HF>());
   ZK_CHECK(hipGetLastError());
-  if (host_io) ZK_CHECK(hipMemcpyAsync(tgt, dt, N * 3 * NP * 8, hipMemcpyDeviceToHost, st));
+  if (host_io) copy_to_host(dev, st, tgt, dt, N * 3 * NP * 8);  // fresh caller arrays: zk_runtime.hpp
   ZK_CHECK(hipStreamSynchronize(st));
 }
 
@@ -1049,7 +1049,7 @@ static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t 
   hipLaunchKernelGGL((k_norm_chunks<C, MODE_PROJ_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, NORM_CHK,
                      (const void *)ds, scratch, dt, exp_p_minus_2<HF>(), 0);
   ZK_CHECK(hipGetLastError());
-  if (host_io) ZK_CHECK(hipMemcpyAsync(tgt, dt, N * 2 * NP * 8, hipMemcpyDeviceToHost, st));
+  if (host_io) copy_to_host(dev, st, tgt, dt, N * 2 * NP * 8);
   ZK_CHECK(hipStreamSynchronize(st));
 }
 
@@ -1196,7 +1196,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   hipLaunchKernelGGL((k_norm_chunks<C, MODE_XYZZ_TO_PROJ>), dim3(div_up(nl, 256)), dim3(256), 0, st, (int)N,
                      NORM_CHK, (const void *)A, nscratch, dt, exp_p_minus_2<HF>(), inverse ? m : 0);
   ZK_CHECK(hipGetLastError());
-  if (host_io) ZK_CHECK(hipMemcpyAsync(tgt, dt, N * 3 * NP * 8, hipMemcpyDeviceToHost, st));
+  if (host_io) copy_to_host(dev, st, tgt, dt, N * 3 * NP * 8);  // fresh caller arrays: zk_runtime.hpp
   ZK_CHECK(hipStreamSynchronize(st));
 }
 

@@ -124,14 +124,13 @@ def load_rocprof_ms(kernel_prefix):
     committed rocprofv3 --stats summary (profiles/*kernel_stats.csv)"""
     import csv
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*kernel_stats.csv")), key=profile_order)
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        for row in csv.DictReader(f):
-            name = row["Name"].replace("void ", "").replace("zk::", "")
-            if name.startswith(kernel_prefix):
-                return {"ms": float(row["AverageNs"]) / 1e6, "calls": int(row["Calls"]),
-                        "source": os.path.relpath(files[-1], ROOT)}
+    for path in reversed(files):  # newest summary that timed this kernel (others profile other legs)
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                name = row["Name"].replace("void ", "").replace("zk::", "")
+                if name.startswith(kernel_prefix):
+                    return {"ms": float(row["AverageNs"]) / 1e6, "calls": int(row["Calls"]),
+                            "source": os.path.relpath(path, ROOT)}
     return None
 
 

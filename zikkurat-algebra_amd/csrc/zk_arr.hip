@@ -107,25 +107,11 @@ __global__ void __launch_bounds__(256) k_arr_map(ArrArgs g) {
 
 // ---------------------------------------------------------------------------- inversion
 
-// x^e (internal form), e = 256-bit exponent, square-and-multiply MSB first (the
+// x^e (internal form), e = 256-bit exponent (sliding window, zk_field.hpp fe_pow_sw; the
 // exponent is the same for every lane: no divergence)
 template <class F>
 __device__ __forceinline__ void fe_pow_int(Fe<F> &r, const Fe<F> &x, const U256 &e) {
-  Fe<F> acc;
-  fe_one(acc);
-  for (int w = 3; w >= 0; w--) {
-    const uint64_t ew = e.w[w];
-    for (int b = 63; b >= 0; b--) {
-      Fe<F> t;
-      fe_sqr(t, acc);
-      acc = t;
-      if ((ew >> b) & 1) {
-        fe_mul(t, acc, x);
-        acc = t;
-      }
-    }
-  }
-  r = acc;
+  fe_pow_sw(r, x, e.w, 4);
 }
 
 // Chunked Montgomery trick: lane t owns elements [t*CHK, (t+1)*CHK).  Pass 1 stores the

@@ -39,23 +39,10 @@ struct W6 {
 template <class F>
 constexpr int xw() { return xyzz_words<F>(); }  // u32 words per stored XYZZ point
 
-// x^e for an NW-word exponent, square-and-multiply MSB first (uniform across lanes)
+// x^e for an NW-word exponent (sliding window, zk_field.hpp fe_pow_sw; uniform across lanes)
 template <class F, int NW>
 __device__ __forceinline__ void fe_pow_words(Fe<F> &r, const Fe<F> &x, const W6 &e) {
-  Fe<F> acc, t;
-  fe_one(acc);
-  for (int w = NW - 1; w >= 0; w--) {
-    const uint64_t ew = e.w[w];
-    for (int b = 63; b >= 0; b--) {
-      fe_sqr(t, acc);
-      acc = t;
-      if ((ew >> b) & 1) {
-        fe_mul(t, acc, x);
-        acc = t;
-      }
-    }
-  }
-  r = acc;
+  fe_pow_sw(r, x, e.w, NW);
 }
 
 template <class F>

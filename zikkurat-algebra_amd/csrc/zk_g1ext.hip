@@ -457,6 +457,18 @@ __device__ ZK_FFT_SCL_ATTR void xyzz_scl(Xyzz<F> &r, const Xyzz<F> &P, const uin
 // multiplies by the integer): BN254 G1 has cofactor 1; BLS12-381 inputs are checked first
 // (k_subgroup_check) and the call falls back to the integer stages when any point fails.
 #include "zk_glv.inc"
+// Waves per SIMD the GLV stage and membership kernels are compiled for (2 caps them at 256 VGPRs
+// so two wavefronts share a SIMD).  BN254 fits 256 with a few spilled registers and gains 8% at
+// 2^18 (57.2 -> 52.7 ms forward, profiles/r05s_fft_two_waves.txt); BLS12-381's kernels hold 445-503
+// VGPRs and spilled 290-420 of them when capped (2^16 forward 25.7 -> 27.6 ms), so they stay at one.
+#ifndef ZK_FFT_WAVES_BN
+#define ZK_FFT_WAVES_BN 2
+#endif
+#ifndef ZK_FFT_WAVES_BLS
+#define ZK_FFT_WAVES_BLS 1
+#endif
+template <class C>
+constexpr int fft_waves() { return C::NP64 == 4 ? ZK_FFT_WAVES_BN : ZK_FFT_WAVES_BLS; }
 
 struct GlvParams {  // decomposition constants of one curve (kernel argument)
   uint64_t g1[4], g2[4], a1[3], b1[3], a2[3], b2[3];
@@ -712,7 +724,7 @@ __device__ __forceinline__ void glv_scl_pair(Xyzz<F> &t, const Xyzz<F> &v, const
 
 // forward DIT stage on lane pairs: pair = butterfly; lane 0 writes u + t, lane 1 u - t
 template <class C>
-__global__ void __launch_bounds__(256) k_fft_fwd_stage_glv(int m, int s, const uint32_t *__restrict__ A,
+__global__ void __launch_bounds__(256, fft_waves<C>()) k_fft_fwd_stage_glv(int m, int s, const uint32_t *__restrict__ A,
                                                            uint32_t *__restrict__ B, const uint64_t *__restrict__ twg,
                                                            W6 beta_ref, uint32_t *__restrict__ scratch, int lanes) {
   using F = typename C::Fp;
@@ -728,7 +740,6 @@ __global__ void __launch_bounds__(256) k_fft_fwd_stage_glv(int m, int s, const u
     const size_t blk = b >> (s - 1), j = b & (half - 1);
     const size_t k0 = (blk << s) + j;
     Xyzz<F> u, v, t;
-    xyzz_load(u, A + k0 * xw<F>());
     xyzz_load(v, A + (k0 + half) * xw<F>());
     if (j == 0) t = v;
     else glv_scl_pair(t, v, twg + (j << (m - s)) * 8, beta, tab);
@@ -737,6 +748,7 @@ __global__ void __launch_bounds__(256) k_fft_fwd_stage_glv(int m, int s, const u
       xyzz_neg(nt, t);
       t = nt;
     }
+    xyzz_load(u, A + k0 * xw<F>());  // read after the multiplication: not live across its chain
     xyzz_add(u, t);
     xyzz_store(B + (k0 + (q ? half : 0)) * xw<F>(), u);
   }
@@ -745,7 +757,7 @@ __global__ void __launch_bounds__(256) k_fft_fwd_stage_glv(int m, int s, const u
 // inverse DIF stage on lane pairs, factor 1/2 per level deferred (k_fft_inv_first_glv applies N^-1
 // once): lane 0 writes u + v, lane 1 (u - v) w^-j
 template <class C>
-__global__ void __launch_bounds__(256) k_fft_inv_stage_glv(int m, int s, const uint32_t *__restrict__ A,
+__global__ void __launch_bounds__(256, fft_waves<C>()) k_fft_inv_stage_glv(int m, int s, const uint32_t *__restrict__ A,
                                                            uint32_t *__restrict__ B, const uint64_t *__restrict__ twg,
                                                            W6 beta_ref, uint32_t *__restrict__ scratch, int lanes) {
   using F = typename C::Fp;
@@ -763,6 +775,11 @@ __global__ void __launch_bounds__(256) k_fft_inv_stage_glv(int m, int s, const u
     Xyzz<F> u, v, d;
     xyzz_load(u, A + k0 * xw<F>());
     xyzz_load(v, A + (k0 + half) * xw<F>());
+    if (q == 0) {  // lane 0's output u + v is written first: u, v are not live across the chain
+      Xyzz<F> w = u;
+      xyzz_add(w, v);
+      xyzz_store(B + k0 * xw<F>(), w);
+    }
     d = u;
     {
       Xyzz<F> nv;
@@ -771,11 +788,7 @@ __global__ void __launch_bounds__(256) k_fft_inv_stage_glv(int m, int s, const u
     }
     Xyzz<F> t = d;
     if (j != 0) glv_scl_pair(t, d, twg + (j << (m - s)) * 8, beta, tab);
-    if (q == 0) {
-      xyzz_add(u, v);
-      t = u;
-    }
-    xyzz_store(B + (k0 + (q ? half : 0)) * xw<F>(), t);
+    if (q) xyzz_store(B + (k0 + half) * xw<F>(), t);
   }
 }
 
@@ -783,7 +796,7 @@ __global__ void __launch_bounds__(256) k_fft_inv_stage_glv(int m, int s, const u
 // per butterfly, pair 0 -> (u + v) N^-1 (dkn), pair 1 -> (u - v) w^-j N^-1 (twn[j], the twiddle
 // with N^-1 folded in) -- one doubled stage instead of a stage plus a scaling pass over N points
 template <class C>
-__global__ void __launch_bounds__(256) k_fft_inv_first_glv(int m, const uint32_t *__restrict__ A,
+__global__ void __launch_bounds__(256, fft_waves<C>()) k_fft_inv_first_glv(int m, const uint32_t *__restrict__ A,
                                                            uint32_t *__restrict__ B, const uint64_t *__restrict__ twn,
                                                            const uint64_t *__restrict__ dkn, W6 beta_ref,
                                                            uint32_t *__restrict__ scratch, int lanes) {
@@ -834,7 +847,7 @@ __device__ __forceinline__ void jac_mul_absz(Jac<F> &r, const Jac<F> &p) {
 // 128 bits on BLS12-381; tools/gen_glv.py checks the test on subgroup and non-subgroup points).
 // bad[block] = 1 when some point of the block fails.
 template <class C>
-__global__ void __launch_bounds__(256) k_subgroup_check(int n, const uint32_t *__restrict__ A, W6 beta_ref, int lanes,
+__global__ void __launch_bounds__(256, fft_waves<C>()) k_subgroup_check(int n, const uint32_t *__restrict__ A, W6 beta_ref, int lanes,
                                                         uint32_t *__restrict__ bad) {
   using F = typename C::Fp;
   Fe<F> beta, t0;
@@ -1012,7 +1025,14 @@ static void batch_from_affine_t(Device &dev, int n, const uint64_t *src, uint64_
   ZK_CHECK(hipStreamSynchronize(st));
 }
 
-static const int NORM_CHK = 32;
+// points per Fermat inversion in k_norm_chunks: each lane's chain is CHK prefix products, one
+// inversion (~490 products) and ~5 products per point on the way back, and the lanes are N / CHK,
+// so small inputs take short chunks (the group FFT's 2^16 points: 16384 lanes of 4 instead of 2048
+// of 32) and large ones keep 32 (the work, N / CHK inversions, stays below the points' own)
+static int norm_chk(size_t N) {
+  const size_t c = N / 16384;
+  return c < 4 ? 4 : (c > 32 ? 32 : (int)c);
+}
 
 template <class C>
 static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
@@ -1032,8 +1052,9 @@ static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t 
     dt = dev.arena.take<uint64_t>(N * 2 * NP);
   }
   uint64_t *scratch = dev.arena.take<uint64_t>(N * NP);
-  const size_t lanes = (N + NORM_CHK - 1) / NORM_CHK;
-  hipLaunchKernelGGL((k_norm_chunks<C, MODE_PROJ_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, NORM_CHK,
+  const int chk = norm_chk(N);
+  const size_t lanes = (N + chk - 1) / chk;
+  hipLaunchKernelGGL((k_norm_chunks<C, MODE_PROJ_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, chk,
                      (const void *)ds, scratch, dt, exp_p_minus_2<HF>(), 0);
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 2 * NP * 8);
@@ -1066,7 +1087,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   glanes = (glanes + 255) & ~(size_t)255;
   const size_t tlanes = std::max(lanes, glanes);
   const size_t nbad = div_up(N, 256);
-  dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 2 * N * xw<F>() * 4 + tlanes * scl_tab_words<F>() * 4 +
+  dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 3 * N * xw<F>() * 4 + tlanes * scl_tab_words<F>() * 4 +
                     tw_cnt * 32 + 2 * tw_cnt * 64 + 64 + nbad * 4 + N * NP * 8 + (1 << 20));
   dev.arena.reset();
   const uint64_t *ds = src;
@@ -1096,17 +1117,28 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   bool glv = glv_on && m > 0;
   const GlvParams gp = glv_params<C>();
   const W6 beta = glv_beta_ref<C>();
+  // BLS12-381: the membership test runs on the context's side stream, on a copy of the loaded
+  // points, BESIDE the GLV stages (speculative: both are one chain per lane at <= one wavefront
+  // per SIMD up to 2^16, so they share the SIMDs' issue slots; before round 5 the stages waited
+  // for it, ~1.2 ms of a 26 ms 2^16 transform).  A point outside the subgroup (the result is
+  // read after the stages) discards the GLV result and reruns the integer stages from the input.
+  uint32_t *hb = nullptr;
+  unsigned cgrid = 0;
   if (glv && C::NP64 == 6) {
-    const unsigned grid = (unsigned)(glanes / 256);
-    hipLaunchKernelGGL(k_subgroup_check<C>, dim3(grid), dim3(256), 0, st, (int)N, A, beta, (int)glanes, bad);
+    uint32_t *Acopy = dev.arena.take<uint32_t>(N * xw<F>());
+    ZK_CHECK(hipMemcpyAsync(Acopy, A, N * xw<F>() * 4, hipMemcpyDeviceToDevice, st));
+    hipEvent_t loaded = dev.split_event(0), checked = dev.split_event(1);
+    ZK_CHECK(hipEventRecord(loaded, st));
+    hipStream_t st2 = dev.aux_stream();
+    ZK_CHECK(hipStreamWaitEvent(st2, loaded, 0));
+    cgrid = (unsigned)(glanes / 256);
+    hipLaunchKernelGGL(k_subgroup_check<C>, dim3(cgrid), dim3(256), 0, st2, (int)N, Acopy, beta, (int)glanes, bad);
     ZK_CHECK(hipGetLastError());
-    uint32_t *hb = reinterpret_cast<uint32_t *>(dev.host_staging(grid * 4 + 64));
-    ZK_CHECK(hipMemcpyAsync(hb, bad, grid * 4, hipMemcpyDeviceToHost, st));
-    ZK_CHECK(hipStreamSynchronize(st));
-    for (unsigned i = 0; i < grid; i++) glv = glv && hb[i] == 0;
+    hb = reinterpret_cast<uint32_t *>(dev.host_staging(cgrid * 4 + 64));
+    ZK_CHECK(hipMemcpyAsync(hb, bad, cgrid * 4, hipMemcpyDeviceToHost, st2));
+    ZK_CHECK(hipEventRecord(checked, st2));
   }
-  g1_fft_last_glv().store(glv ? 1 : 0);
-  if (glv) {
+  auto run_glv = [&] {
     // twiddles (decomposed): forward w^e; inverse (w^-1)^e with the 1/2 per level deferred to one
     // multiplication by N^-1 folded into the first stage (on the subgroup the m halvings = N^-1)
     zkh::Fe<HR> g, one, ninv;
@@ -1147,8 +1179,9 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
       ZK_CHECK(hipGetLastError());
       std::swap(in, out);
     }
-    A = in;
-  } else if (m > 0) {
+    return in;
+  };
+  auto run_int = [&] {
     // twiddles: forward w^e; inverse (w^-1)^e / 2 -- the reference's gpow sequences
     // (G1_proj.c:705-711, 758-764), canonical Fr, standard form
     zkh::Fe<HR> g, scale;
@@ -1173,15 +1206,38 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
       else
         hipLaunchKernelGGL(k_fft_fwd_stage<C>, dim3(grid), dim3(256), 0, st, m, s, in, out, tw, scratch, (int)lanes);
       ZK_CHECK(hipGetLastError());
-      uint32_t *x = in;
-      in = out;
-      out = x;
+      std::swap(in, out);
     }
-    A = in;
+    return in;
+  };
+  if (glv) {
+    uint32_t *res = run_glv();
+    if (hb) {  // the speculative membership test's verdict
+      const hipEvent_t checked = dev.split_event(1);
+      for (;;) {
+        const hipError_t e = hipEventQuery(checked);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) ZK_CHECK(e);
+        std::this_thread::yield();
+      }
+      for (unsigned i = 0; i < cgrid; i++) glv = glv && hb[i] == 0;
+    }
+    if (glv) {
+      A = res;
+    } else {  // some point lies outside the r-subgroup: the reference's exact integer schedule
+      ZK_CHECK(hipStreamSynchronize(st));
+      hipLaunchKernelGGL(k_fft_load<C>, dim3(div_up(N, 256)), dim3(256), 0, st, (int)N, inverse ? 0 : m, ds, A);
+      ZK_CHECK(hipGetLastError());
+      A = run_int();
+    }
+  } else if (m > 0) {
+    A = run_int();
   }
-  const size_t nl = (N + NORM_CHK - 1) / NORM_CHK;
+  g1_fft_last_glv().store(glv ? 1 : 0);
+  const int chk = norm_chk(N);
+  const size_t nl = (N + chk - 1) / chk;
   hipLaunchKernelGGL((k_norm_chunks<C, MODE_XYZZ_TO_PROJ>), dim3(div_up(nl, 256)), dim3(256), 0, st, (int)N,
-                     NORM_CHK, (const void *)A, nscratch, dt, exp_p_minus_2<HF>(), inverse ? m : 0);
+                     chk, (const void *)A, nscratch, dt, exp_p_minus_2<HF>(), inverse ? m : 0);
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 3 * NP * 8);  // fresh caller arrays: zk_runtime.hpp
   ZK_CHECK(hipStreamSynchronize(st));

@@ -427,7 +427,18 @@ static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64
   uint64_t *dt = sg.out(tgt, N);
   if (N) {
     if (op == ARR_INV || op == ARR_DIV) {
-      const int CHK = 32;
+      // elements per Fermat inversion: a lane's chain is ~6 products per element plus one
+      // inversion (323 products with the sliding window), the work N (6 + 323 / CHK); the lanes
+      // N / CHK are sized to ZK_INV_LANES (default 131072: two wavefronts per SIMD at 164 VGPRs),
+      // CHK within [8, 128] (2^24: 128 -> 8.5 products per element instead of 16 at CHK 32; inv
+      // 2.64 -> 1.94 ms, div 2.35 -> 1.86 ms through the host wrapper, profiles/r05u_*)
+      static const size_t inv_lanes = [] {
+        const char *e = getenv("ZK_INV_LANES");
+        const long v = e ? atol(e) : 0;
+        return v > 0 ? (size_t)v : (size_t)131072;
+      }();
+      const size_t cq = N / inv_lanes;
+      const int CHK = cq < 8 ? 8 : (cq > 128 ? 128 : (int)cq);
       uint64_t *scratch = dev.arena.take<uint64_t>(N * 4);
       uint32_t *flag = dev.arena.take<uint32_t>(1);
       ZK_CHECK(hipMemsetAsync(flag, 0, 4, st));

@@ -1026,12 +1026,20 @@ static void batch_from_affine_t(Device &dev, int n, const uint64_t *src, uint64_
 }
 
 // points per Fermat inversion in k_norm_chunks: each lane's chain is CHK prefix products, one
-// inversion (~490 products) and ~5 products per point on the way back, and the lanes are N / CHK,
-// so small inputs take short chunks (the group FFT's 2^16 points: 16384 lanes of 4 instead of 2048
-// of 32) and large ones keep 32 (the work, N / CHK inversions, stays below the points' own)
+// inversion (~490 products) and ~5 products per point on the way back, and the lanes are N / CHK.
+// The kernel is latency-bound on that chain (one wavefront per SIMD at 248-254 VGPRs already
+// issues most of what a SIMD can), so CHK keeps ~one wavefront per SIMD busy: N / ZK_NORM_LANES
+// (default 65536) within [2, 32] -- 2^16 points: 2 (the group FFT), 2^20: 16.  Measured
+// (profiles/r05u_inversion_chunks.txt): 2^20 0.95 ms at 32, 0.81 at 16, 1.16 at 8; 2^16 0.541 at
+// 4, 0.528 at 2, 0.553 at 1.
 static int norm_chk(size_t N) {
-  const size_t c = N / 16384;
-  return c < 4 ? 4 : (c > 32 ? 32 : (int)c);
+  static const size_t target = [] {
+    const char *e = getenv("ZK_NORM_LANES");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (size_t)v : (size_t)65536;
+  }();
+  const size_t c = N / target;
+  return c < 2 ? 2 : (c > 32 ? 32 : (int)c);
 }
 
 template <class C>

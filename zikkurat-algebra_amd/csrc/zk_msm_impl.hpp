@@ -543,11 +543,14 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 #ifndef ZK_ACCUM_WAVES14
 #define ZK_ACCUM_WAVES14 2  // the 381-bit madd (A/B hook: 3 spilled ~56 VGPRs in round 2)
 #endif
+#ifndef ZK_ACCUM_WAVES20
+#define ZK_ACCUM_WAVES20 2  // BN254 G2 (Fp2 over 10-limb Fp)
+#endif
 template <class F>
 struct AccumOcc {  // minimum waves per SIMD k_accum is compiled for
   // 254-bit lazy madd: 3 waves (153 VGPRs); at 4 it spills 30 VGPRs inside the loop (1.49 vs
   // 1.44 ms at BN128 2^20, profiles/r02at_bn128_lazy_madd.txt)
-  static constexpr int waves = F::N >= 28 ? 1 : (F::N >= 14 ? ZK_ACCUM_WAVES14 : 3);
+  static constexpr int waves = F::N >= 28 ? 1 : (F::N > 14 ? ZK_ACCUM_WAVES20 : (F::N == 14 ? ZK_ACCUM_WAVES14 : 3));
 };
 
 template <class C>

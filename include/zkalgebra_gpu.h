@@ -318,6 +318,12 @@ ZKG_API void zkg_msm_set_group_limit(size_t entries);
  * Y-sum lanes fill several rounds of the chip: c = 20 from 2^23 pairs), 0: always k_ysum2,
  * 1: always k_ysum3 (block-level shapes, c >= 12) */
 ZKG_API void zkg_msm_set_ysum_mode(int mode);
+/* test hook: device-resident G1/G2 MSMs of at least 2^lg pairs whose windows fit one pass run as
+ * two window groups with both bucket sorts on a second stream (B's beside A's accumulation);
+ * lg = 0 disables it, lg < 0 restores the default: from 2^23 pairs (or the environment's
+ * ZK_MSM_AHEAD_MIN) for the curves whose accumulation leaves VGPRs for the sort (BN128 G1), off
+ * otherwise */
+ZKG_API void zkg_msm_set_ahead_min(int lg);
 /* test hook: NTT pass split -- 12: two passes of 2^9..2^12-point DFTs (4096-element tiles) for
  * every 2^17..2^24; 8: passes of <= 2^8-point DFTs only; 0: the default (two passes at 2^20 only) */
 ZKG_API void zkg_ntt_set_max_radix(int r);

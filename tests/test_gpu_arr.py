@@ -70,6 +70,31 @@ def test_batch_inversion(gpu, oracle, curve, n):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+def test_batch_inversion_2_24_ragged(gpu, oracle, curve):
+    """the prover-size chunking (128 elements per Fermat inversion from 2^24, zk_arr.hip) with a
+    ragged last chunk: inv(b) b == 1 everywhere, sampled elements equal the oracle's inverses,
+    and a zero in the LAST chunk still zeroes every output"""
+    n = (1 << 24) + 4099
+    b = fr(gpu, curve, 97, n)
+    db, dt = gpu.DeviceBuffer(b), gpu.DeviceBuffer.empty(b.nbytes)
+    try:
+        gpu.arr_op_device(curve, "inv", n, db, None, d_tgt=dt)
+        inv = dt.to_host(b)
+        idx = np.r_[0, 1, 127, 128, np.arange(n - 4100, n, 97), n - 1]
+        assert np.array_equal(inv[idx], oracle.arr_op(curve, "inv", len(idx), np.ascontiguousarray(b[idx])))
+        gpu.arr_op_device(curve, "mul", n, dt, db, d_tgt=dt)
+        assert gpu.arr_is_one(curve, dt.to_host(b))
+        b[n - 2] = 0
+        db.free()
+        db = gpu.DeviceBuffer(b)
+        gpu.arr_op_device(curve, "inv", n, db, None, d_tgt=dt)
+        assert not dt.to_host(b).any()
+    finally:
+        for d in (db, dt):
+            d.free()
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_batch_inversion_zero_rule(gpu, curve):
     """reference batch_inv (Fr_mont.c:258-285): one zero input zeroes EVERY output"""
     b = fr(gpu, curve, 71, 5000)

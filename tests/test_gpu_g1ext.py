@@ -39,7 +39,7 @@ def test_batch_from_affine(gpu, reference, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
-@pytest.mark.parametrize("n", [1, 31, 33, 1000, 1 << 16])
+@pytest.mark.parametrize("n", [1, 31, 33, 1000, 1 << 16, (1 << 20) + 37])  # 2^20 + 37: 16 points per inversion, ragged
 def test_batch_to_affine(gpu, oracle, reference, curve, n):
     proj = projective(gpu, oracle, curve, n, 102 + n) if n <= 1000 else None
     if proj is None:  # large: cheap inputs (Z = 1 after from_affine, plus infinities)

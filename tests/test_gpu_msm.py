@@ -309,3 +309,30 @@ def test_ysum_kernels_vs_oracle(gpu, oracle, curve, mode, window, n):
     finally:
         gpu.msm_set_ysum_mode(-1)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("window,n", [(0, 5000), (13, 9001), (16, 70000), (20, 20000), (0, (1 << 18) + 5)])
+def test_sort_ahead_groups_vs_oracle(gpu, oracle, curve, window, n):
+    """the sort-ahead shape -- two window groups with both sorts on the second stream (by default
+    from 2^23 device-resident BN128 pairs) -- forced down to small inputs: equal to the oracle,
+    to the plain pipeline and to the default, odd window counts included"""
+    sc = gpu.gen_fr(curve, 900 + window, n)
+    pts = gpu.gen_points(curve, 901 + window, n)
+    pts[::113] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    ds, dp = gpu.DeviceBuffer(sc), gpu.DeviceBuffer(pts)
+    try:
+        gpu.msm_set_ahead_min(0)
+        one = gpu.msm_device(curve, n, ds, dp, window=window)
+        gpu.msm_set_ahead_min(12)
+        two = gpu.msm_device(curve, n, ds, dp, window=window)
+        assert gpu.msm_last_groups() == 2
+        gpu.msm_set_ahead_min(-1)
+        dflt = gpu.msm_device(curve, n, ds, dp, window=window)
+    finally:
+        gpu.msm_set_ahead_min(-1)
+        ds.free()
+        dp.free()
+    assert np.array_equal(one, two) and np.array_equal(one, dflt)
+    want = oracle.normalize(curve, oracle.msm(curve, sc, pts, mont=True, out="proj"))
+    assert np.array_equal(oracle.normalize(curve, two), want)

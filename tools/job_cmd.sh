@@ -1,9 +1,8 @@
-# r05v: BN254 G2 k_accum at one wave per SIMD (349 VGPRs, no spill; variant g2bn1) vs two (256, 178 spilled); inversion chunk defaults
+# r05y: one-group sort beside the point conversion (device-resident, from 2^18) + BN128 two-group sort-ahead
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-echo "== in-tree (ZK_ACCUM_WAVES20=2)"
-timeout -k 10 300 python3 tools/g2_time.py bn128 || exit 1
-echo "== g2bn1 (ZK_ACCUM_WAVES20=1)"
-ZK_LIB_PATH=variants/g2bn1/libzkalgebra_gpu.so timeout -k 10 300 python3 tools/g2_time.py bn128 || exit 1
-echo "== in-tree defaults: inversion chunks"
-timeout -k 10 120 python3 tools/inv_probe.py || exit 1
+for m in 20 24; do
+  echo "== bls 2^$m off"; ZK_MSM_AHEAD_MIN=0 timeout -k 10 200 python3 tools/sweep_window.py bls12_381 $m || exit 1
+  echo "== bls 2^$m default"; timeout -k 10 200 python3 tools/sweep_window.py bls12_381 $m || exit 1
+done
+echo "== bn 2^24 default"; timeout -k 10 200 python3 tools/sweep_window.py bn128 24 || exit 1

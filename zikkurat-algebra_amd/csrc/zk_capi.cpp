@@ -299,6 +299,7 @@ ZKG_API int zkg_msm_window(int curve, int npoints, int expo_nlimbs, int expos_mo
 ZKG_API void zkg_msm_profile(int on) { zk::msm_set_profile(on); }
 ZKG_API void zkg_msm_set_group_limit(size_t entries) { zk::msm_set_group_limit(entries); }
 ZKG_API void zkg_msm_set_ysum_mode(int mode) { zk::msm_set_ysum_mode(mode); }
+ZKG_API void zkg_msm_set_ahead_min(int lg) { zk::msm_set_ahead_min(lg); }
 ZKG_API void zkg_ntt_set_max_radix(int r) { zk::ntt_set_max_radix(r); }
 
 ZKG_API void zkg_ntt_set_table_max(size_t entries) { zk::ntt_set_table_max(entries); }

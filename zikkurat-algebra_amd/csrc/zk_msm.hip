@@ -41,6 +41,7 @@ int msm_default_window_bits(int n, int bits) {
 }
 
 void msm_set_ysum_mode(int mode) { ysum_mode().store(mode < 0 ? -1 : (mode ? 1 : 0)); }
+void msm_set_ahead_min(int lg) { msm_ahead_min().store(lg < 0 ? -1 : lg); }
 void msm_set_profile(int on) { msm_profile_flag().store(on); }
 int msm_last_groups_read() { return msm_last_groups().load(); }
 void msm_set_group_limit(size_t entries) {

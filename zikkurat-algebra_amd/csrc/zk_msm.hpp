@@ -33,6 +33,7 @@ int msm_default_window_bits(int n, int bits);  // G1: the window for `bits`-bit 
 void msm_set_profile(int on);  // per-phase event timing of every MSM call, printed to stderr
 void msm_set_group_limit(size_t entries);  // test hook: max sorted entries per pipeline pass (0: default)
 void msm_set_ysum_mode(int mode);          // test hook: G1 Y-sum kernel (-1 auto, 0 k_ysum2, 1 k_ysum3)
+void msm_set_ahead_min(int lg);           // test hook: sort-ahead from 2^lg device-resident pairs (0 off, < 0 default)
 int msm_last_groups_read();  // window groups of the most recent msm_run (degrade-path tests)
 
 // scalars: n x nl u64 (Montgomery Fr if mont, else plain integers of 64 nl bits, any nl >= 1)

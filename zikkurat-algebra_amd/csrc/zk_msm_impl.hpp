@@ -1524,6 +1524,9 @@ static int msm_splits(int n, bool host_inputs, bool one_pass) {
 #ifndef ZK_YSUM_PF
 #define ZK_YSUM_PF 1  // k_ysum2 loads the next bucket one iteration ahead
 #endif
+#ifndef ZK_YSUM_PF_G2
+#define ZK_YSUM_PF_G2 1  // the same for Fp2 points (A/B hook)
+#endif
 // Y sums by k_ysum3 (two waves per SIMD, LDS prefetch) when the lanes fill several rounds of one
 // wave per SIMD (ZK_YSUM3_LANES, default 4 x 65536: c = 20 from 2^23 pairs).  Mode -1: that rule,
 // 0 / 1: always k_ysum2 / k_ysum3 (block-level shapes); set by the environment ZK_YSUM3 (A/B hook)
@@ -1777,6 +1780,9 @@ struct GroupPass {
   void *cubtmp_sort = nullptr;
   const uint64_t *pts_ref = nullptr;
   std::vector<hipEvent_t> sorted_ev;
+  // sort-ahead (msm_run, large device-resident inputs): the pass was sorted on another stream,
+  // which records this event; launch() waits for it instead of sorting
+  hipEvent_t presorted = nullptr;
   // stitch state (level ping-pong)
   const uint32_t *inK, *inV;
   size_t slots;
@@ -2004,7 +2010,8 @@ struct GroupPass {
                              s.W, c, s.l0, s.r0, s.r1, Y);
       }
       if (!two_waves)
-        hipLaunchKernelGGL((k_ysum2<C, ZK_YSUM_PF != 0>), dim3(nblk), dim3(256), 0, st, buckets, offsets,
+        hipLaunchKernelGGL((k_ysum2<C, is_base_field<F>() ? ZK_YSUM_PF != 0 : ZK_YSUM_PF_G2 != 0>), dim3(nblk),
+                           dim3(256), 0, st, buckets, offsets,
                            (const uint8_t *)filled, s.W, c, s.l0, s.r0, s.r1, Y);
     } else {  // small shapes: in-wavefront segments
       const size_t lanes = (size_t)s.W * s.ylanes;
@@ -2027,7 +2034,9 @@ struct GroupPass {
   // the next split starts from complete buckets without the host looking at any count.
   void launch() {
     for (int sp = 0; sp < s.NS; sp++) {
-      if (sst) {  // split sp's sort on the sort stream, beside split sp-1's accumulation
+      if (presorted) {  // one split (msm_run's sort-ahead shape)
+        ZK_CHECK(hipStreamWaitEvent(st, presorted, 0));
+      } else if (sst) {  // split sp's sort on the sort stream, beside split sp-1's accumulation
         wait_for(sst, wait_sc, ready_sc, sp);
         sort(sp, sst, cubtmp_sort);
         ZK_CHECK(hipEventRecord(sorted_ev[sp], sst));
@@ -2204,6 +2213,37 @@ static void msm_run_bits(Device &dev, int n, const ScalarSlice &sc_in, const uin
   prof.report(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
+// Sort-ahead: device-resident inputs of at least 2^ZK_MSM_AHEAD_MIN pairs (default 23; read once,
+// A/B hook) whose windows fit one pass run as TWO window groups whose bucket sorts both go to the
+// context's sort stream: group A's beside the point conversion, group B's beside group A's
+// accumulation.  Window groups are independent sums, so unlike point splits this adds no
+// additions.  It pays only where k_accum leaves VGPRs free for the sort's wavefronts: the 254-bit
+// madd at three waves per SIMD (153 VGPRs) -- BN128 2^24 26.97 -> 26.35 ms -- while the 381-bit
+// one fills the register file at two (2 x 254): there the sort waits for accumulation waves to
+// retire and the accumulation grows by what the sort saved (BLS12-381 2^23 22.53 / 22.63 ms, 2^24
+// 39.94 / 39.99, profiles/r05x_sort_ahead.txt).  Below 2^23 the halved Y-sum / job-sum / stitch
+// launches (latency-bound at c = 16) cost about what the hidden sort saves.
+inline int msm_ahead_default() {
+  static const int v = [] {
+    const char *e = getenv("ZK_MSM_AHEAD_MIN");
+    return e ? atoi(e) : 23;
+  }();
+  return v;
+}
+inline std::atomic<int> &msm_ahead_min() {  // zkg_msm_set_ahead_min (test hook): < 0 the default
+  static std::atomic<int> v{-1};
+  return v;
+}
+// (Sorting ONE group on the sort stream beside the point conversion measured no better: BLS12-381
+// 2^20 3.565 vs 3.506 ms, 2^24 39.23 vs 39.34 ms, profiles/r05x_sort_ahead.txt.)
+template <class C>
+static bool msm_ahead(int n, bool host_inputs, int W, int Wg) {
+  if (host_inputs || Wg != W || W < 2) return false;
+  const int set = msm_ahead_min().load();  // the test hook applies to every field
+  const int lg = set >= 0 ? set : (AccumOcc<typename C::Fp>::waves >= 3 ? msm_ahead_default() : 0);
+  return lg > 0 && lg < 31 && (size_t)n >= ((size_t)1 << lg);
+}
+
 // Run the device pipeline for one scalar slice.  points are DEVICE pointers (or host
 // pointers when host_inputs, in which case they are staged, with the scalars).
 // Result: sum_i k_i P_i in host XYZZ (reference Montgomery form).
@@ -2244,7 +2284,11 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   // and accumulated as soon as its scalars and points have landed while the next split's cross PCIe
   auto splits = [&](int wg) { return msm_splits(n, host_inputs, wg == W); };
   MsmShape s = make_shape(n, c, Wg, splits(Wg));
-  while (!dev.arena.try_reserve(sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(s))) {
+  const int Wa = (W + 1) / 2;
+  const bool ahead = msm_ahead<C>(n, host_inputs, W, Wg) &&
+                     dev.arena.try_reserve(int_bytes + 3 * 256 + group_bytes<C>(make_shape(n, c, Wa, 1)) +
+                                           group_bytes<C>(make_shape(n, c, W - Wa, 1)));
+  while (!ahead && !dev.arena.try_reserve(sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(s))) {
     if (!dropped_twiddles) {
       ZK_CHECK(hipStreamSynchronize(st));
       ntt_release(dev);
@@ -2256,7 +2300,7 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
     s = make_shape(n, c, Wg, splits(Wg));
   }
   const int NS = s.NS;
-  msm_last_groups().store((W + Wg - 1) / Wg);
+  msm_last_groups().store(ahead ? 2 : (W + Wg - 1) / Wg);
   dev.arena.reset();
   ScalarSlice sc = sc_in;
   uint32_t *pts_int = nullptr;
@@ -2317,6 +2361,7 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
     inputs_on_aux = true;
   } else {
     pts_int = dev.arena.take<uint32_t>((size_t)n * aff_words<F>());
+    if (ahead) ZK_CHECK(hipEventRecord(dev.split_event(0), st));  // the sorts start behind the caller's work
     hipLaunchKernelGGL(k_points_int<C>, dim3(div_up(n, 256)), dim3(256), 0, st, points, n, pts_int);
     ZK_CHECK(hipGetLastError());
   }
@@ -2324,6 +2369,26 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
   const size_t mark = dev.arena.used();
   const size_t per_w = (size_t)c * 4 * C::NP64;  // exported u64 per window
   uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging((size_t)W * per_w * 8 + 64));
+  if (ahead) {
+    GroupPass<C> pa(dev, make_shape(n, c, Wa, 1), sc, 0, pts_int, h, &prof, st, 0);
+    GroupPass<C> pb(dev, make_shape(n, c, W - Wa, 1), sc, Wa, pts_int, h + (size_t)Wa * per_w, &prof, st, 1);
+    hipStream_t sst = dev.aux2_stream();
+    ZK_CHECK(hipStreamWaitEvent(sst, dev.split_event(0), 0));
+    pa.sort(0, sst, pa.cubtmp);
+    ZK_CHECK(hipEventRecord(dev.split_event(1), sst));
+    pb.sort(0, sst, pb.cubtmp);
+    ZK_CHECK(hipEventRecord(dev.split_event(2), sst));
+    pa.presorted = dev.split_event(1);
+    pb.presorted = dev.split_event(2);
+    pa.launch();
+    pb.launch();  // waits for B's sort: every sort-stream kernel is complete before pb.finish()
+    pb.finish();
+    timer_collect(dev);
+    const auto t0 = std::chrono::steady_clock::now();
+    finish_host<C>(c, W, h, out);
+    prof.report(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    return;
+  }
   // Window groups run one after the other on the device's stream.  (Running two groups
   // concurrently on two streams -- one's sort and latency-bound tail beside the other's
   // accumulation -- was measured and does not pay: the two accumulations overlap each
@@ -2383,6 +2448,10 @@ size_t msm_workspace_bytes(int n, int nl, bool mont, bool host_inputs, int windo
   const size_t pt_bytes = host_inputs ? (size_t)n * 2 * C::NP64 * 8 : 0;
   const size_t int_bytes = (size_t)n * aff_words<F>() * 4;
   const int NS = msm_splits(n, host_inputs, Wg == W);
+  if (msm_ahead<C>(n, host_inputs, W, Wg)) {
+    const int Wa = (W + 1) / 2;
+    return int_bytes + 3 * 256 + group_bytes<C>(make_shape(n, c, Wa, 1)) + group_bytes<C>(make_shape(n, c, W - Wa, 1));
+  }
   return sc_bytes + pt_bytes + int_bytes + 3 * 256 + group_bytes<C>(make_shape(n, c, Wg, NS));
 }
 

@@ -59,7 +59,7 @@ EXTENSION_SYMBOLS = [
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_msm_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
     "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
     "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
-    "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_msm_set_ysum_mode", "zkg_ntt_set_max_radix", "zkg_ntt_set_table_max",
+    "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_msm_set_ysum_mode", "zkg_msm_set_ahead_min", "zkg_ntt_set_max_radix", "zkg_ntt_set_table_max",
     "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_g1_fft_last_glv", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
     "zkg_release", "zkg_comm_unique_id", "zkg_comm_init", "zkg_comm_destroy", "zkg_comm_rank", "zkg_comm_world",
     "zkg_comm_allgather", "zkg_comm_barrier", "zkg_comm_max_f64", "zkg_g1_comm_sum_partials",
@@ -551,6 +551,11 @@ def msm_profile(on):
 def msm_set_ysum_mode(mode):
     """test hook: G1 Y-sum kernel (-1 by size, 0 k_ysum2, 1 k_ysum3)"""
     load().zkg_msm_set_ysum_mode(int(mode))
+
+
+def msm_set_ahead_min(lg):
+    """test hook: sort-ahead window groups from 2^lg device-resident pairs (0 off, -1 default)"""
+    load().zkg_msm_set_ahead_min(int(lg))
 
 
 def msm_set_group_limit(entries):

@@ -1,8 +1,14 @@
-# r05y: one-group sort beside the point conversion (device-resident, from 2^18) + BN128 two-group sort-ahead
+# r05za: level-1/1.5 sort chunk (entries staged in LDS per round): 4096 (in-tree) vs 8192 vs 16384
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-for m in 20 24; do
-  echo "== bls 2^$m off"; ZK_MSM_AHEAD_MIN=0 timeout -k 10 200 python3 tools/sweep_window.py bls12_381 $m || exit 1
-  echo "== bls 2^$m default"; timeout -k 10 200 python3 tools/sweep_window.py bls12_381 $m || exit 1
+O=gpurun_out/${TAG}
+for v in base sc8k sc16k; do
+  L=""; [ $v != base ] && L=variants/$v/libzkalgebra_gpu.so
+  echo "== $v"
+  for m in 20 23 24; do
+    ZK_LIB_PATH=$L timeout -k 10 200 python3 tools/sweep_window.py bls12_381 $m || exit 1
+  done
+  ZK_LIB_PATH=$L timeout -k 10 200 python3 tools/sweep_window.py bn128 24 || exit 1
+  ZK_LIB_PATH=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${O}_$v -o run --output-format csv -- \
+    python3 tools/sweep_window.py bls12_381 24 > ${O}_$v.log 2>&1 || exit 1
 done
-echo "== bn 2^24 default"; timeout -k 10 200 python3 tools/sweep_window.py bn128 24 || exit 1

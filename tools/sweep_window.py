@@ -3,6 +3,7 @@
    python tools/sweep_window.py bls12_381 20 13 14 15 16 17   # device-resident MSM per window size
    python tools/sweep_window.py phases                          # per-phase profile at several sizes
 """
+import hashlib
 import os
 import sys
 import time
@@ -33,7 +34,8 @@ def run(curve, logn, windows, reps=5, profile=False):
         kms, kn = zk.timer(enable=False)
         zk.msm_profile(False)
         print(f"{curve} 2^{logn} c={c or zk.load().zkg_msm_window(zk.CURVE_ID[curve], n, 4, 1)}: {dt*1e3:.3f} ms/msm "
-              f"({n/dt:.3e} pairs/s), accum {kms/kn:.3f} ms", flush=True)
+              f"({n/dt:.3e} pairs/s), accum {kms/kn:.3f} ms, result {hashlib.sha256(r.tobytes()).hexdigest()[:12]}",
+              flush=True)
     ds.free()
     dp.free()
 

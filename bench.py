@@ -282,11 +282,13 @@ def launch_ranks(n, argv, script=None, grace_s=10.0):
                                           stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
                                           text=True))
 
-        def pump():  # rank 0's stdout, line by line, to ours
+        def pump():  # rank 0's stdout, line by line: the JSON line to ours, anything else (a
+            # library's own chatter, e.g. gloo's "connected to 1 peer ranks") to stderr
             for line in procs[0].stdout:
                 lines.append(line)
-                sys.stdout.write(line)
-                sys.stdout.flush()
+                out = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+                out.write(line)
+                out.flush()
 
         t = threading.Thread(target=pump, daemon=True)
         t.start()

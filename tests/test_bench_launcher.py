@@ -29,6 +29,8 @@ STUB = textwrap.dedent("""
     if mode == "silent":
         sys.exit(0)
     if rank == 0:
+        if mode == "chatty":  # a library printing to stdout (gloo's peer-connection line)
+            print("[Gloo] Rank 0 is connected to 1 peer ranks.", flush=True)
         print(json.dumps({"metric": "stub", "n_gpus": world, "value": 1.0}), flush=True)
 """)
 
@@ -93,3 +95,13 @@ def test_real_bench_ranks_fail_loudly_without_gpu():
     p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {})
     assert p.returncode != 0
     assert not p.stdout.strip()
+
+
+def test_launcher_stdout_is_the_json_line_only(tmp_path):
+    """rank 0's non-JSON stdout (gloo prints its peer-connection line there) goes to stderr, so
+    the launcher's stdout is exactly the one result line"""
+    p, _ = _launch(tmp_path, 2, "chatty")
+    assert p.returncode == 0, p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2
+    assert "[Gloo]" in p.stderr

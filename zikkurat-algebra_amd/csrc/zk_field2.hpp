@@ -101,21 +101,39 @@ __device__ __forceinline__ void fe_mul3(Fe<F2<B>> &r, const Fe<F2<B>> &a) {
   fe_add(t, a, a);
   fe_add(r, t, a);
 }
-// Karatsuba: a0 b0, a1 b1, (a0 + a1)(b0 + b1)
+#ifndef ZK_FP2_LAZY
+#define ZK_FP2_LAZY 1  // 0: three full Montgomery products (A/B hook)
+#endif
+// c0 = a0 b0 - a1 b1, c1 = a0 b1 + a1 b0 as two shared-reduction pairs (fe_mul2: the column sums of
+// two products, one Montgomery reduction): c0 = REDC(a0 b0 + a1 (2p - b1)), c1 = REDC(a0 b1 + a1 b0).
+// Four limb products and two reductions instead of Karatsuba's three products and three
+// reductions, and none of its five exact additions / subtractions (each two carry chains).
+// Operands < 2p with normalised limbs (what every G2 producer -- the exact add / sub / mul --
+// gives) -> both pairs < 8p^2 < p R' (R'/p = 2^11 on BLS12-381, 2^7.4 on BN254), outputs < 2p,
+// columns as fe_mul2's (zk_params.inc asserts their bound).  tests/test_fp2_lazy.py runs a
+// bit-level model of it against big-integer Fp2 arithmetic on extreme operands.
 template <class B>
 __device__ __forceinline__ void fe_mul(Fe<F2<B>> &r, const Fe<F2<B>> &a, const Fe<F2<B>> &b) {
-  Fe<B> a0, a1, b0, b1, t0, t1, s, u, r0, r1;
+  Fe<B> a0, a1, b0, b1, r0, r1;
   f2_split(a0, a1, a);
   f2_split(b0, b1, b);
+#if ZK_FP2_LAZY
+  Fe<B> nb1;
+  fe_sub_lazy<B, 2, 1>(nb1, Fe<B>{}, b1);  // 2p - b1, in (0, 2p]
+  fe_norm(nb1);
+  fe_mul2(r0, a0, b0, a1, nb1);  // schoolbook streaming pairs: the Karatsuba-column form (fe_mul2k)
+  fe_mul2(r1, a0, b1, a1, b0);   // held two column arrays and spilled ~360 VGPRs in the G2 madd
+#else
+  Fe<B> t0, t1, s, u, m;
   fe_mul(t0, a0, b0);
   fe_mul(t1, a1, b1);
   fe_add(s, a0, a1);
   fe_add(u, b0, b1);
-  Fe<B> m;
   fe_mul(m, s, u);
   fe_sub(r0, t0, t1);
   fe_sub(m, m, t0);
   fe_sub(r1, m, t1);
+#endif
   f2_join(r, r0, r1);
 }
 // (a0 + a1 u)^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u

@@ -522,6 +522,92 @@ def scalar_redc(F):
     F.canon(F.mul(x, kstd, "fe_ref_to_std"), "fe_ref_to_std canon")
 
 
+JAC_X = 10  # Jacobian accumulator / table-entry invariant of the lazy group-FFT routines: X < 10p
+
+
+def jac_form(F):
+    """zk_g1ext.hip (ZK_FFT_LAZY): X < JAC_X p, Y, Z < 2p, normalised limbs"""
+    return {"X": F.norm_val(JAC_X * F.p, "X"), "Y": F.norm_val(2 * F.p, "Y"), "Z": F.norm_val(2 * F.p, "Z")}
+
+
+def in_jac_form(F, pt, what):
+    form = jac_form(F)
+    for k in ("X", "Y", "Z"):
+        F.need(F.is_norm(pt[k]) and pt[k].val <= form[k].val,
+               f"{what}: output {k} < {F.units(pt[k]):.2f} p outside the Jacobian form (< {F.units(form[k]):.0f} p)")
+
+
+def jac_dbl_lazy(F):
+    """zk_g1ext.hip jac_dbl, ZK_FFT_LAZY (both base fields): dbl-2009-l with the multiples folded into
+    products and lazy differences; Y3 one shared-reduction pair"""
+    tag = "jac_dbl_lazy"
+    pt = jac_form(F)
+    A = F.sqr(pt["X"], tag + " A")
+    B = F.sqr(pt["Y"], tag + " B")
+    x4 = F.add_lazy(pt["X"], pt["X"], tag + " 2X")
+    x4 = F.add_lazy(x4, x4, tag + " 4X")
+    D = F.mulk(x4, B, tag + " D")
+    E = F.add_lazy(F.add_lazy(A, A, tag + " 2A"), A, tag + " E")
+    if F.N == 9:  # fe_norm on the 29-bit limbs only
+        E = F.norm(E, tag + " E")
+    F2 = F.sqr(E, tag + " F")
+    t = F.add_lazy(D, D, tag + " 2D")
+    X3 = F.norm(F.sub_lazy(F2, t, 8, 2, tag + " X3"), tag + " X3")
+    y2 = F.add_lazy(pt["Y"], pt["Y"], tag + " 2Y")
+    Z3 = F.mulk(y2, pt["Z"], tag + " Z3")
+    t = F.norm(F.sub_lazy(D, X3, JAC_X, 1, tag + " D-X3"), tag + " D-X3")
+    nb = F.norm(F.sub_lazy(F.zero(), B, 2, 1, tag + " 2p-B"), tag + " 2p-B")
+    nb8 = F.add_lazy(nb, nb, tag + " 2nb")
+    nb8 = F.add_lazy(nb8, nb8, tag + " 4nb")
+    nb8 = F.add_lazy(nb8, nb8, tag + " 8nb")
+    if F.N == 9:
+        nb8 = F.norm(nb8, tag + " 8nb")
+    Y3 = F.mul2k(E, t, nb8, B, tag + " Y3")
+    in_jac_form(F, {"X": X3, "Y": Y3, "Z": Z3}, tag)
+    F.log.append(f"{tag}: 4X < {F.units(x4):.0f} p, E < {F.units(E):.0f} p, X3 < {F.units(X3):.1f} p, "
+                 f"Y3 < {F.units(Y3):.2f} p, Z3 < {F.units(Z3):.2f} p")
+
+
+def jac_add_cached_lazy(F):
+    """zk_g1ext.hip jac_add_cached, ZK_FFT_LAZY: add-1998-cmo-2 with the table entry's Z^2, Z^3
+    cached (products), H and r exact (zero-tested), the rest lazy"""
+    tag = "jac_add_cached_lazy"
+    acc = jac_form(F)
+    b = jac_form(F)
+    b["ZZ"] = F.sqr(b["Z"], tag + " ZZ")
+    b["ZZZ"] = F.mul(b["ZZ"], b["Z"], tag + " ZZZ")
+    # lane 1's lookup: X times beta (a product), Y possibly negated (exact fe_neg)
+    b["X"] = F.mulk(b["X"], F.norm_val(2 * F.p, "beta"), tag + " beta X")
+    b["Y"] = F.sub(F.zero(), b["Y"], tag + " -Y")
+    Z1Z1 = F.sqr(acc["Z"], tag + " Z1Z1")
+    U1 = F.mulk(acc["X"], b["ZZ"], tag + " U1")
+    U2 = F.mulk(b["X"], Z1Z1, tag + " U2")
+    S1 = F.mulk(acc["Y"], b["ZZZ"], tag + " S1")
+    t = F.mulk(acc["Z"], Z1Z1, tag + " Z1^3")
+    S2 = F.mulk(b["Y"], t, tag + " S2")
+    H = F.sub(U2, U1, tag + " H")
+    r = F.sub(S2, S1, tag + " r")
+    F.is_zero_ok(H, tag + " H")
+    F.is_zero_ok(r, tag + " r")
+    HH = F.sqr(H, tag + " HH")
+    HHH = F.mulk(H, HH, tag + " HHH")
+    V_ = F.mulk(U1, HH, tag + " V")
+    RR = F.sqr(r, tag + " RR")
+    t = F.sub_lazy(RR, HHH, 2, 1, tag + " RR-HHH")
+    v2 = F.add_lazy(V_, V_, tag + " 2V")
+    X3 = F.norm(F.sub_lazy(t, v2, 6, 2, tag + " X3"), tag + " X3")
+    t = F.norm(F.sub_lazy(V_, X3, JAC_X + 2, 1, tag + " V-X3"), tag + " V-X3")
+    nS1 = F.norm(F.sub_lazy(F.zero(), S1, 2, 1, tag + " 2p-S1"), tag + " 2p-S1")
+    Y3 = F.mul2k(r, t, nS1, HHH, tag + " Y3")
+    t = F.mulk(acc["Z"], b["Z"], tag + " Z1Z2")
+    Z3 = F.mulk(t, H, tag + " Z3")
+    in_jac_form(F, {"X": X3, "Y": Y3, "Z": Z3}, tag)
+    # the accumulator converted to XYZZ (jac_to_xyzz) keeps X; xyzz_add / the normalisation only
+    # multiply it: every product of a value < JAC_X p by one < 2p is in range
+    F.mulk(X3, F.norm_val(2 * F.p), tag + " consumers of X")
+    F.log.append(f"{tag}: X3 < {F.units(X3):.1f} p, V - X3 < {F.units(t):.1f} p, Y3 < {F.units(Y3):.2f} p")
+
+
 def check_bn254():
     F = Field("bn254_fp")
     madd_lazy9(F)
@@ -533,8 +619,8 @@ def check_bn254():
 def run_all(verbose=True):
     ok = True
     results = []
-    plans = [("bls12_381_fp", [madd_lazy14, add_lazy, add_exact_on_stored]),
-             ("bn254_fp", [madd_lazy9, add_lazy, add_exact_on_stored]),
+    plans = [("bls12_381_fp", [madd_lazy14, add_lazy, add_exact_on_stored, jac_dbl_lazy, jac_add_cached_lazy]),
+             ("bn254_fp", [madd_lazy9, add_lazy, add_exact_on_stored, jac_dbl_lazy, jac_add_cached_lazy]),
              ("bls12_381_fr", [ntt_paths, scalar_redc]),
              ("bn254_fr", [ntt_paths, scalar_redc])]
     for name, fns in plans:

@@ -231,8 +231,49 @@ __device__ __forceinline__ void fft_mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b
   fe_mul(r, a, b);
 #endif
 }
+// Lazy form (ZK_FFT_LAZY, default, both base fields): the doubling and the cached addition take no
+// exact addition / subtraction (each two carry chains, ~56 issue slots) except the two whose
+// results are tested for zero (the addition's H and r): multiples are folded into products (4X B,
+// (2Y) Z), differences are a + K p - b (fe_sub_lazy) re-normalised where a product takes them.
+// Invariant of a Jacobian accumulator / table entry: X < 10p, Y, Z < 2p, normalised limbs (every
+// consumer of X multiplies it: the XYZZ it is converted to keeps X < 10p, which xyzz_add and the
+// normalisation only multiply).  tools/lazy_bounds.py (jac_dbl_lazy, jac_add_cached_lazy) replays
+// both routines on that invariant: outputs X < 9p, Y, Z < 1.02p, every column < 2^64.
+#ifndef ZK_FFT_LAZY
+#define ZK_FFT_LAZY 1
+#endif
 template <class F>
 __device__ __forceinline__ void jac_dbl(Jac<F> &p) {  // in place; infinity stays infinity
+#if ZK_FFT_LAZY
+  if constexpr (F::N == 14 || (F::N == 9 && F::RB == 29)) {
+    Fe<F> A, B, D, E, F2, X3, t, x4, y2, nb, nb8;
+    fe_sqr(A, p.X);                        // X < 10p
+    fe_sqr(B, p.Y);
+    fe_add_lazy(x4, p.X, p.X);
+    fe_add_lazy(x4, x4, x4);               // 4X < 40p, limbs < 2^30
+    fe_mulk(D, x4, B);                     // D = 4 X B
+    fe_add_lazy(E, A, A);
+    fe_add_lazy(E, E, A);                  // E = 3A < 6p
+    if constexpr (F::N == 9) fe_norm(E);  // 29-bit limbs: the doubled limbs of the square
+    fe_sqr(F2, E);                         // F = E^2
+    fe_add_lazy(t, D, D);                  // 2D < 4p
+    fe_sub_lazy<F, 8, 2>(X3, F2, t);       // X3 = F - 2D < 9p
+    fe_norm(X3);
+    fe_add_lazy(y2, p.Y, p.Y);
+    fe_mulk(p.Z, y2, p.Z);                 // Z3 = (2Y) Z
+    fe_sub_lazy<F, 10, 1>(t, D, X3);       // D - X3 < 12p
+    fe_norm(t);
+    fe_sub_lazy<F, 2, 1>(nb, Fe<F>{}, B);  // 2p - B
+    fe_norm(nb);
+    fe_add_lazy(nb8, nb, nb);
+    fe_add_lazy(nb8, nb8, nb8);
+    fe_add_lazy(nb8, nb8, nb8);            // 8 (2p - B) < 16p
+    if constexpr (F::N == 9) fe_norm(nb8);  // 29-bit limbs: 8x would reach 2^32
+    fe_mul2k(p.Y, E, t, nb8, B);           // Y3 = E (D - X3) - 8 B^2
+    p.X = X3;
+    return;
+  }
+#endif
 #if ZK_FFT_DBL2
   Fe<F> A, B, D, E, F2, X3, t, u;
   fe_sqr(A, p.X);
@@ -322,6 +363,25 @@ __device__ __forceinline__ void jac_add_cached(Jac<F> &acc, const JacC<F> &b) {
   fe_sqr(HH, H);
   fft_mul(HHH, H, HH);
   fft_mul(V, U1, HH);
+#if ZK_FFT_LAZY
+  if constexpr (F::N == 14 || (F::N == 9 && F::RB == 29)) {
+    Fe<F> RR, v2, nS1;
+    fe_sqr(RR, r);
+    fe_sub_lazy<F, 2, 1>(t, RR, HHH);      // RR - HHH < 4p
+    fe_add_lazy(v2, V, V);
+    fe_sub_lazy<F, 6, 2>(X3, t, v2);       // X3 = r^2 - HHH - 2V < 9p
+    fe_norm(X3);
+    fe_sub_lazy<F, 12, 1>(t, V, X3);       // V - X3 < 14p
+    fe_norm(t);
+    fe_sub_lazy<F, 2, 1>(nS1, Fe<F>{}, S1);
+    fe_norm(nS1);
+    fe_mul2k(acc.Y, r, t, nS1, HHH);       // Y3 = r (V - X3) - S1 HHH
+    fft_mul(t, acc.Z, b.Z);
+    fft_mul(acc.Z, t, H);                  // Z3 = Z1 Z2 H
+    acc.X = X3;
+    return;
+  }
+#endif
   fe_sqr(t, r);
   fe_sub(t, t, HHH);
   fe_sub(t, t, V);

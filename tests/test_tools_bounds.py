@@ -15,13 +15,29 @@ def _load(name):
 
 
 def test_lazy_bounds_all_paths():
-    """every lazy path (both MSM base fields' mixed and full additions, the NTT butterflies of
-    every radix, the closing reductions, the scalar REDC) satisfies its limb / value bounds"""
+    """every lazy path (both MSM base fields' mixed and full additions, the group FFT's lazy
+    Jacobian doubling and cached addition on both base fields, the NTT butterflies of every radix,
+    the closing reductions, the scalar REDC) satisfies its limb / value bounds"""
     spec, mod = _load("lazy_bounds")
     spec.loader.exec_module(mod)
     ok, results = mod.run_all(verbose=False)
     assert ok, [r for r in results if r[2] != "ok"]
-    assert len(results) == 10
+    assert len(results) == 14
+    assert {fn for _, fn, _ in results} >= {"jac_dbl_lazy", "jac_add_cached_lazy"}
+
+
+def test_lazy_jacobian_checker_rejects_a_tight_constant():
+    """the Jacobian replays are not vacuous: with the accumulator invariant X < 10p a difference
+    D + 4p - X3 (too small a K) must be rejected"""
+    spec, mod = _load("lazy_bounds")
+    spec.loader.exec_module(mod)
+    F = mod.Field("bls12_381_fp")
+    D, X3 = F.norm_val(2 * F.p), F.norm_val(9 * F.p)
+    try:
+        F.sub_lazy(D, X3, 4, 1)
+        raise AssertionError("D + 4p - X3 accepted for X3 < 9p")
+    except mod.BoundError:
+        pass
 
 
 def test_lazy_bounds_catch_a_broken_invariant():

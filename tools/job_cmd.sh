@@ -1,7 +1,4 @@
-# r05ze: lazy Jacobian doubling / cached addition in the BLS12-381 group FFT (ZK_FFT_LAZY)
+# r05zj: lazy Fp2 squaring (ZK_FP2_LAZY) -- G2 MSM timings (before: r05zd 2.18 / 5.39 (BN128), 4.66 / 11.95 ms (BLS12-381))
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/${TAG}
-timeout -k 10 120 python3 tools/fft_time.py 16 3 || exit 1
-timeout -k 10 200 python3 tools/fft_time.py 18 2 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace -d ${O}_trace -o run --output-format csv -- python3 tools/fft_time.py 16 1 > ${O}_trace.log 2>&1 || exit 1
+timeout -k 10 300 python3 tools/g2_time.py || exit 1

@@ -42,6 +42,96 @@ def projective_points(zk, oracle, curve, n, seed, n_inf=3):
     return out
 
 
+def jacobian_points(zk, oracle, curve, n, seed, n_inf=3, affine=None):
+    """n Jacobian points (X:Y:Z) = (x l^2 : y l^3 : l) with random l (the generator's points, or the
+    given affine rows), a few at infinity as the reference's Jacobian infinity (l^2 : l^3 : 0)
+    (Y^2 = X^3, X, Y != 0: bls12_381_G1_jac.c:164-180).  Deterministic, like projective_points."""
+    import ctypes
+    import random
+
+    def ptr(a):
+        return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    NP = zk.NLIMBS_P[curve]
+    aff = zk.gen_points(curve, seed, n) if affine is None else affine
+    lam = zk.gen_points(curve, seed + 1, n)[:, :NP]  # random field elements (canonical)
+    out = np.zeros((n, 3 * NP), dtype=np.uint64)
+    fid = FP_ID[curve]
+    for i in range(n):
+        l1 = np.ascontiguousarray(lam[i])
+        l2 = np.zeros(NP, dtype=np.uint64)
+        l3 = np.zeros(NP, dtype=np.uint64)
+        oracle.lib.zko_fmul(fid, ptr(l1), ptr(l1), ptr(l2))
+        oracle.lib.zko_fmul(fid, ptr(l2), ptr(l1), ptr(l3))
+        for k, lk in ((0, l2), (1, l3)):
+            x = np.ascontiguousarray(aff[i, k * NP:(k + 1) * NP])
+            o = np.zeros(NP, dtype=np.uint64)
+            oracle.lib.zko_fmul(fid, ptr(x), ptr(lk), ptr(o))
+            out[i, k * NP:(k + 1) * NP] = o
+        out[i, 2 * NP:] = l1
+    rng = random.Random(seed)
+    for i in rng.sample(range(n), min(n_inf, n)):
+        l1 = np.ascontiguousarray(lam[i])
+        l2 = np.zeros(NP, dtype=np.uint64)
+        l3 = np.zeros(NP, dtype=np.uint64)
+        oracle.lib.zko_fmul(fid, ptr(l1), ptr(l1), ptr(l2))
+        oracle.lib.zko_fmul(fid, ptr(l2), ptr(l1), ptr(l3))
+        out[i, :NP] = l2
+        out[i, NP:2 * NP] = l3
+        out[i, 2 * NP:] = 0
+    return out
+
+
+def g2_points(reflib, curve, n, k0=12345, k1=67890, n_inf=0, seed=0):
+    """n DISTINCT affine G2 points P0 + i H (P0 = k0 G, H = k1 G, the reference's own G2 generator,
+    scl_small, add and batch_to_affine: oracle/_ref), n_inf of them replaced by the all-0xFF
+    affine infinity at positions drawn with `seed`.  Used by the G2 tests and tools/make_golden.py."""
+    import ctypes
+    import random
+    NP = {"bn128": 4, "bls12_381": 6}[curve]
+    lib = reflib
+    gen = np.ctypeslib.as_array((ctypes.c_uint64 * (6 * NP)).in_dll(lib, f"{curve}_G2_proj_gen_G2")).copy()
+    scl = getattr(lib, f"{curve}_G2_proj_scl_small")
+    scl.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    p0, h = np.zeros(6 * NP, np.uint64), np.zeros(6 * NP, np.uint64)
+    scl(k0, gen.ctypes.data, p0.ctypes.data)
+    scl(k1, gen.ctypes.data, h.ctypes.data)
+    proj = np.zeros((n, 6 * NP), np.uint64)
+    add = getattr(lib, f"{curve}_G2_proj_add")
+    add.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    if n:
+        proj[0] = p0
+    hp = h.ctypes.data
+    base = proj.ctypes.data
+    row = 6 * NP * 8
+    for i in range(1, n):
+        add(base + (i - 1) * row, hp, base + i * row)
+    aff = np.zeros((n, 4 * NP), np.uint64)
+    f = getattr(lib, f"{curve}_G2_proj_batch_to_affine")
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    f(n, proj.ctypes.data, aff.ctypes.data)
+    if n_inf:
+        rng = random.Random(seed)
+        aff[rng.sample(range(n), n_inf)] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    return aff
+
+
+def g2_case_inputs(reflib, curve, logn, seed, gen_fr):
+    """scalars (Montgomery, 1/1000 zero rows) and 2^logn distinct affine G2 points (1/4096 at
+    infinity) of one tools/make_golden.py G2_CASES row; shared by the generator and the tests"""
+    n = 1 << logn
+    pts = g2_points(reflib, curve, n, k0=seed & 0xFFFF, k1=(seed >> 4) + 77, n_inf=n >> 12, seed=seed)
+    sc = gen_fr(curve, seed, n)
+    rng = np.random.default_rng(seed)
+    sc[rng.choice(n, n // 1000, replace=False)] = 0
+    return sc, pts
+
+
+def g2_large_golden():
+    """reference G2 MSM outputs at 2^16 / 2^18 (tools/make_golden.py g2large)"""
+    p = os.path.join(GOLD, "g2_msm.json")
+    return json.load(open(p)) if os.path.exists(p) else {}
+
+
 def bls_nonsubgroup_points(n, seed):
     """random affine points of E(Fp): y^2 = x^3 + 4, almost surely outside the order-r subgroup
     (cofactor h ~ 2^126); Montgomery form (R = 2^384)"""

@@ -41,10 +41,11 @@ class _FakeLib:
         return 0
 
 
-def _rank(rank, world, key, rdir, q, nonce=None):
+def _rank(rank, world, key, rdir, q, nonce=None, env=None):
     sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
     os.environ["ZKG_RDZV_KEY"] = key
     os.environ["ZKG_RDZV_DIR"] = rdir
+    os.environ.update(env or {})
     if nonce:
         os.environ["ZKG_RDZV_NONCE"] = nonce
     import sharded
@@ -130,3 +131,39 @@ def test_multi_rank_without_torchrun_or_key_fails_fast(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "2")
     with pytest.raises(RuntimeError, match="ZKG_RDZV_KEY"):
         sharded.rendezvous_path()
+
+
+def _agent(rank, world, key, rdir, q, env):
+    """one node's elastic agent: its rank is its child, so every rank has a different parent pid"""
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_rank, args=(rank, world, key, rdir, q, None, env))
+    p.start()
+    p.join(timeout=120)
+    sys.exit(p.exitcode or 0)
+
+
+def test_torchrun_nonce_is_the_same_on_every_node(tmp_path):
+    """multi-node torchrun: ZKG_RDZV_KEY + a shared ZKG_RDZV_DIR, no ZKG_RDZV_NONCE, each rank the
+    child of its own agent (different parent pids): the torchrun nonce (run id, restart count) must
+    match on every rank, or the ranks on other nodes never accept rank 0's id"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    env = {"TORCHELASTIC_RUN_ID": "job-42", "TORCHELASTIC_RESTART_COUNT": "0"}
+    agents = [ctx.Process(target=_agent, args=(r, 3, "multinode", str(tmp_path), q, env)) for r in range(3)]
+    for a in agents:
+        a.start()
+    got = [q.get(timeout=120)[1] for _ in agents]
+    for a in agents:
+        a.join(timeout=60)
+        assert a.exitcode == 0
+    assert len({g[2] for g in got}) == 1
+    assert sorted(g[0] for g in got) == [0, 1, 2]
+
+
+def test_torchrun_nonce_has_no_process_ids(monkeypatch):
+    sys.path.insert(0, os.path.join(ROOT, "zikkurat-algebra_amd"))
+    import sharded
+    monkeypatch.delenv("ZKG_RDZV_NONCE", raising=False)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "abc")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "2")
+    assert sharded.rendezvous_nonce() == b"abc:2"

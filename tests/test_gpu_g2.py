@@ -3,36 +3,19 @@
 bit-exact against the reference's own C (oracle/_ref).  Test points are built with the
 reference library itself: an arithmetic progression P0 + i H of generator multiples,
 converted by its batch_to_affine."""
-import ctypes
+import hashlib
 
 import numpy as np
 import pytest
+
+import golden_io
 
 pytestmark = pytest.mark.gpu
 CURVES = ["bn128", "bls12_381"]
 
 
 def g2_points(reference, curve, n, k0=12345, k1=67890):
-    NP = {"bn128": 4, "bls12_381": 6}[curve]
-    lib = reference.lib
-    gen = np.ctypeslib.as_array((ctypes.c_uint64 * (6 * NP)).in_dll(lib, f"{curve}_G2_proj_gen_G2")).copy()
-    scl = getattr(lib, f"{curve}_G2_proj_scl_small")
-    scl.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
-    p0, h = np.zeros(6 * NP, np.uint64), np.zeros(6 * NP, np.uint64)
-    scl(k0, gen.ctypes.data, p0.ctypes.data)
-    scl(k1, gen.ctypes.data, h.ctypes.data)
-    proj = np.zeros((n, 6 * NP), np.uint64)
-    add = getattr(lib, f"{curve}_G2_proj_add")
-    cur = p0.copy()
-    for i in range(n):
-        proj[i] = cur
-        nxt = np.zeros_like(cur)
-        add(cur.ctypes.data_as(ctypes.c_void_p), h.ctypes.data_as(ctypes.c_void_p),
-            nxt.ctypes.data_as(ctypes.c_void_p))
-        cur = nxt
-    aff = np.zeros((n, 4 * NP), np.uint64)
-    reference.arr(curve, "G2_proj_batch_to_affine", n, proj, aff)
-    return aff
+    return golden_io.g2_points(reference.lib, curve, n, k0, k1)
 
 
 def ref_msm(reference, curve, sc, pts, mont, affine):
@@ -96,3 +79,30 @@ def test_g2_msm_linearity_large(gpu, points, curve):
     lhs = gpu.g2_msm(curve, ab, pts, affine=True)
     rhs = gpu.g2_msm(curve, np.concatenate([a, b]), np.concatenate([pts, pts]), affine=True)
     assert np.array_equal(lhs, rhs)
+
+
+# ---------------------------------------------------------------------------- bench sizes (round 6)
+G2L = golden_io.g2_large_golden()
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("key", sorted(G2L))
+def test_g2_msm_vs_reference_at_bench_sizes(gpu, oracle, reference, key):
+    """2^16 and 2^18 DISTINCT points on both curves (the sizes bench_ext times: large windows, the
+    G2 bucket sort and Y sums), with infinities and zero scalars, against the reference's own
+    <C>_G2_proj_MSM_mont_coeff_affine_out (tools/make_golden.py g2large); at 2^16 also the std entry
+    with a 2^256 - 1 scalar row (used verbatim)"""
+    g = G2L[key]
+    curve = g["curve"]
+    sc, pts = golden_io.g2_case_inputs(reference.lib, curve, g["log_n"], g["seed"], gpu.gen_fr)
+    assert _sha(sc) == g["scalars_sha256"] and _sha(pts) == g["points_sha256"]
+    got = gpu.g2_msm(curve, sc, pts, affine=True)
+    assert [int(x) for x in got] == g["mont_affine"], key
+    if "std_affine_row3_all_ones" in g:
+        std = oracle.to_std({"bn128": 1, "bls12_381": 3}[curve], sc)
+        std[3] = np.uint64(0xFFFFFFFFFFFFFFFF)
+        got = gpu.g2_msm(curve, std, pts, std=True, affine=True)
+        assert [int(x) for x in got] == g["std_affine_row3_all_ones"], key

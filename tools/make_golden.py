@@ -14,6 +14,9 @@ independent restatement in oracle/zk_oracle.c is checked equal by the tests).
                                         # points with random Z; BLS12-381 non-subgroup points at m = 10):
                                         # reference forward / inverse SHA-256 digests
                                         # -> tests/golden/group_fft.json      ~1 min, 8 cores
+  python tools/make_golden.py groupfft m16  # only the keys containing "m16" (others kept)
+  python tools/make_golden.py g2large   # G2 MSM at 2^16 / 2^18 (distinct points, infinities, zero
+                                        # scalars), both curves -> tests/golden/g2_msm.json   ~2 min
   python tools/make_golden.py patterns  # adversarial NTT inputs (tests/golden_io.py NTT_PATTERNS) at
                                         # m = 5, 12, 14, 20 and random 2^20 vectors: reference forward /
                                         # inverse SHA-256 digests -> tests/golden/ntt_patterns.json   ~1 min
@@ -259,6 +262,14 @@ GFFT_CASES = [  # (key, curve, m, input kind, seed, infinities)
     ("bls12_381_m12", "bls12_381", 12, "subgroup_projective", 0x6F1012, 3),
     ("bls12_381_m14", "bls12_381", 14, "subgroup_projective", 0x6F1014, 5),
     ("bls12_381_nonsubgroup_m10", "bls12_381", 10, "nonsubgroup_affine", 0x6F200A, 0),
+    # round 6: the bench size m = 16, and the Jacobian twins <C>_G1_jac_fft_* (bls12_381_G1_jac.c:727-838)
+    ("bn128_m16", "bn128", 16, "subgroup_projective", 0x6F0016, 7),
+    ("bls12_381_m16", "bls12_381", 16, "subgroup_projective", 0x6F1016, 7),
+    ("jac_bn128_m12", "bn128", 12, "subgroup_jacobian", 0x6F3012, 3),
+    ("jac_bn128_m14", "bn128", 14, "subgroup_jacobian", 0x6F3014, 5),
+    ("jac_bls12_381_m12", "bls12_381", 12, "subgroup_jacobian", 0x6F4012, 3),
+    ("jac_bls12_381_m14", "bls12_381", 14, "subgroup_jacobian", 0x6F4014, 5),
+    ("jac_bls12_381_nonsubgroup_m10", "bls12_381", 10, "nonsubgroup_jacobian", 0x6F500A, 2),
 ]
 
 
@@ -267,6 +278,11 @@ def _gfft_input(case):
     n = 1 << m
     if kind == "subgroup_projective":
         return golden_io.projective_points(zk, Oracle(), curve, n, seed, n_inf=n_inf)
+    if kind == "subgroup_jacobian":
+        return golden_io.jacobian_points(zk, Oracle(), curve, n, seed, n_inf=n_inf)
+    if kind == "nonsubgroup_jacobian":
+        return golden_io.jacobian_points(zk, Oracle(), curve, n, seed, n_inf=n_inf,
+                                         affine=golden_io.bls_nonsubgroup_points(n, seed))
     aff = golden_io.bls_nonsubgroup_points(n, seed)
     out = np.zeros((n, 3 * zk.NLIMBS_P[curve]), dtype=np.uint64)
     Reference().arr(curve, "G1_proj_batch_from_affine", n, aff, out)
@@ -280,19 +296,25 @@ def _gfft_job(args):
     g = zk.get_fft_subgroup(curve, m).gen_array()
     out = np.zeros_like(pts)
     t = time.time()
-    Reference().arr(curve, "G1_proj_fft_inverse" if inverse else "G1_proj_fft_forward", m, g, pts, out)
+    co = "jac" if "jacobian" in case[3] else "proj"
+    Reference().arr(curve, f"G1_{co}_fft_inverse" if inverse else f"G1_{co}_fft_forward", m, g, pts, out)
     return key, inverse, sha(pts), sha(out), time.time() - t
 
 
-def make_group_fft():
+def make_group_fft(only=None):
+    """only: comma-separated substring filter on the case keys; other cases keep their stored digests"""
     os.makedirs(GOLD, exist_ok=True)
-    with mp.Pool(8) as pool:
-        res = pool.map(_gfft_job, [(c, inv) for c in GFFT_CASES for inv in (False, True)])
-    data = {}
-    for case in GFFT_CASES:
+    cases = [c for c in GFFT_CASES if not only or any(o in c[0] for o in only.split(","))]
+    jobs = sorted([(c, inv) for c in cases for inv in (False, True)], key=lambda j: -(j[0][2] + j[1]))
+    with mp.Pool(8) as pool:  # longest first
+        res = pool.map(_gfft_job, jobs, chunksize=1)
+    path = os.path.join(GOLD, "group_fft.json")
+    data = json.load(open(path)) if os.path.exists(path) else {}
+    for case in cases:
         key, curve, m, kind, seed, n_inf = case
-        d = {"curve": curve, "log_n": m, "input": kind, "seed": seed, "n_inf": n_inf,
-             "reference": "<C>_G1_proj_fft_forward / _inverse of lib/cbits (bls12_381_G1_proj.c:679-790)"}
+        src = ("<C>_G1_jac_fft_forward / _inverse of lib/cbits (bls12_381_G1_jac.c:727-838)" if "jacobian" in kind
+               else "<C>_G1_proj_fft_forward / _inverse of lib/cbits (bls12_381_G1_proj.c:679-790)")
+        d = {"curve": curve, "log_n": m, "input": kind, "seed": seed, "n_inf": n_inf, "reference": src}
         for k, inv, sin, sout, dt in res:
             if k != key:
                 continue
@@ -302,7 +324,46 @@ def make_group_fft():
         data[key] = d
         print(key, "forward %.1fs inverse %.1fs" % (d["reference_forward_seconds"], d["reference_inverse_seconds"]),
               flush=True)
-    json.dump(data, open(os.path.join(GOLD, "group_fft.json"), "w"), indent=1, sort_keys=True)
+    json.dump(data, open(path, "w"), indent=1, sort_keys=True)
+
+
+# ----------------------------------------------------------------------------- G2 MSM at bench sizes
+
+G2_CASES = [  # (key, curve, log n, seed): distinct points P0 + i H, 1/4096 of them infinity, 1/1000 zero scalars
+    ("bn128_2^16", "bn128", 16, 0x6A0016),
+    ("bn128_2^18", "bn128", 18, 0x6A0018),
+    ("bls12_381_2^16", "bls12_381", 16, 0x6A1016),
+    ("bls12_381_2^18", "bls12_381", 18, 0x6A1018),
+]
+
+
+def _g2_job(case):
+    key, curve, logn, seed = case
+    ref = Reference()
+    sc, pts = golden_io.g2_case_inputs(ref.lib, curve, logn, seed, zk.gen_fr)
+    NP = zk.NLIMBS_P[curve]
+    out = np.zeros(4 * NP, dtype=np.uint64)
+    t = time.time()
+    ref.arr(curve, "G2_proj_MSM_mont_coeff_affine_out", sc.shape[0], sc, pts, out, 4)
+    dt = time.time() - t
+    std = Oracle().to_std(FLD_FR[curve], sc) if logn == 16 else None
+    res = {"curve": curve, "log_n": logn, "seed": seed, "scalars_sha256": sha(sc), "points_sha256": sha(pts),
+           "mont_affine": [int(x) for x in out], "reference_seconds": dt,
+           "reference": f"{curve}_G2_proj_MSM_mont_coeff_affine_out (bls12_381_G2_proj.c:498 ff.)"}
+    if std is not None:  # the std entry on to_std'd scalars with a 2^256 - 1 row (used verbatim)
+        std[3] = np.uint64(0xFFFFFFFFFFFFFFFF)
+        o2 = np.zeros(4 * NP, dtype=np.uint64)
+        ref.arr(curve, "G2_proj_MSM_std_coeff_affine_out", std.shape[0], std, pts, o2, 4)
+        res["std_affine_row3_all_ones"] = [int(x) for x in o2]
+    return key, res
+
+
+def make_g2_large():
+    with mp.Pool(4) as pool:
+        res = dict(pool.map(_g2_job, G2_CASES, chunksize=1))
+    json.dump(res, open(os.path.join(GOLD, "g2_msm.json"), "w"), indent=1, sort_keys=True)
+    for k, v in res.items():
+        print(k, "reference %.1fs" % v["reference_seconds"], flush=True)
 
 
 def make_large(which):
@@ -330,7 +391,7 @@ def make_large(which):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) < 2 or sys.argv[1] not in ("small", "large", "patterns", "groupfft"):
+    if len(sys.argv) < 2 or sys.argv[1] not in ("small", "large", "patterns", "groupfft", "g2large"):
         print(__doc__)
         sys.exit(2)
     if sys.argv[1] == "small":
@@ -338,6 +399,8 @@ if __name__ == "__main__":
     elif sys.argv[1] == "patterns":
         make_patterns()
     elif sys.argv[1] == "groupfft":
-        make_group_fft()
+        make_group_fft(sys.argv[2] if len(sys.argv) > 2 else None)
+    elif sys.argv[1] == "g2large":
+        make_g2_large()
     else:
         make_large(sys.argv[2] if len(sys.argv) > 2 else None)

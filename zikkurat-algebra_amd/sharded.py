@@ -80,14 +80,16 @@ def rendezvous_path():
 def rendezvous_nonce():
     """per-launch tag written after the id: a rank accepts only an id file carrying its own
     launch's tag, so a stale file left by an earlier launch with the same key is never used.
-    ZKG_RDZV_NONCE (bench.py's launcher), else torchrun's run id and restart count; empty (no
-    check) otherwise."""
+    ZKG_RDZV_NONCE (bench.py's launcher), else torchrun's run id and restart count -- the same on
+    every node of a launch (each node's elastic agent is a different process, so nothing per-process
+    may enter it: ADVICE r05); empty (no check) otherwise.  With torchrun's default run id ("none")
+    the tag does not tell launches apart; rank 0's removal of the old file and the per-launch key
+    then carry that."""
     n = os.environ.get("ZKG_RDZV_NONCE")
     if n:
         return n.encode()
     if "TORCHELASTIC_RUN_ID" in os.environ:
-        return (f"{os.environ['TORCHELASTIC_RUN_ID']}:{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}:"
-                f"{os.getppid()}").encode()
+        return f"{os.environ['TORCHELASTIC_RUN_ID']}:{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}".encode()
     return b""
 
 

@@ -761,9 +761,10 @@ def end_to_end(zk, curve, scalars, points, device_ms, ntt, args, device_aff, rep
                          "pcie_GBps_effective": 2 * x.nbytes / max(dt2 - dev * 1e-3, 1e-9) / 1e9,
                          "note": "ms: a fresh, uninitialised output array per call (np.empty, as the binding's "
                                  "mallocForeignPtrArray, Poly.hs:405): its first touch -- 512 MiB of new pages -- "
-                                 "is paid inside the call, where the library's helper threads prefault it during "
-                                 "the input copy and the passes; ms_reused_output: the same symbol into a resident "
-                                 "buffer.  (Round 4 allocated with np.zeros inside the timing: +~25 ms of calloc "
+                                 "is paid inside the call: the library copies the result back through its own pinned "
+                                 "double buffer (copy_to_host, zk_runtime.cpp: 32 MiB DMA pieces into one half while "
+                                 "the host pool copies the other half into the caller's array, faulting its pages in "
+                                 "as it goes); ms_reused_output: the same symbol into a resident buffer.  (Round 4 allocated with np.zeros inside the timing: +~25 ms of calloc "
                                  "zeroing that the Haskell binding never pays.)"}
     return out
 

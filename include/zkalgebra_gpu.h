@@ -108,6 +108,21 @@ ZKG_API void bls12_381_G1_proj_batch_to_affine  ( int N, const uint64_t *src , u
 ZKG_API void bls12_381_G1_proj_fft_forward( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
 ZKG_API void bls12_381_G1_proj_fft_inverse( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
 
+/* Jacobian twins (round 6): bls12_381_G1_jac.h:9-10, 48-49 (bn128_G1_jac.h same lines); bound by the
+ * Jacobian G1 instance -- batchFromAffine / batchToAffine (G1/Jac.hs:374-389; Curve.msm on Jac.G1 is
+ * msmJac cs gs = msm cs (batchToAffine gs), Jac.hs:188, 220) and forwardFFT / inverseFFT = curveFFT /
+ * curveIFFT (Jac.hs:189-190, 264-291).  Conventions: affine infinity -> (1 : 1 : 0)
+ * (bls12_381_G1_jac.c:108-116, 183-187); Z = 0 -> all-0xFF (to_affine, :120-125); FFT outputs
+ * normalised (x : y : 1), infinity (0 : 1 : 0) (jac normalize, :62-67, applied at :773-775, :835-837). */
+ZKG_API void bn128_G1_jac_batch_from_affine( int N, const uint64_t *src , uint64_t *tgt );
+ZKG_API void bn128_G1_jac_batch_to_affine  ( int N, const uint64_t *src , uint64_t *tgt );
+ZKG_API void bn128_G1_jac_fft_forward( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bn128_G1_jac_fft_inverse( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_G1_jac_batch_from_affine( int N, const uint64_t *src , uint64_t *tgt );
+ZKG_API void bls12_381_G1_jac_batch_to_affine  ( int N, const uint64_t *src , uint64_t *tgt );
+ZKG_API void bls12_381_G1_jac_fft_forward( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
+ZKG_API void bls12_381_G1_jac_fft_inverse( int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt );
+
 /* Fr vector operations around the NTT.  <C> in {bn128, bls12_381}.
  *   lib/cbits/curves/array/mont/bls12_381_arr_mont.h:3-48 (bn128_arr_mont.h same lines),
  *   bound by Haskell ZK.Algebra.Curves.<C>.Array (Array.hs:108-352).
@@ -289,6 +304,10 @@ ZKG_API int zkg_poly_div_by_vanishing_device(int curve, int n1, const uint64_t *
 ZKG_API void zkg_g1_fft_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src,
                                uint64_t *d_tgt);
 ZKG_API void zkg_g1_batch_to_affine_device(int curve, int n, const uint64_t *d_src, uint64_t *d_tgt);
+/* the same on Jacobian rows (the <C>_G1_jac_fft_* / _batch_to_affine conventions above) */
+ZKG_API void zkg_g1_jac_fft_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src,
+                                   uint64_t *d_tgt);
+ZKG_API void zkg_g1_jac_batch_to_affine_device(int curve, int n, const uint64_t *d_src, uint64_t *d_tgt);
 
 /* host helpers on G1 (projective, reference Montgomery form) */
 ZKG_API void zkg_g1_proj_add(int curve, const uint64_t *a, const uint64_t *b, uint64_t *out);

@@ -57,6 +57,7 @@ def test_reference_signatures_match_reference_headers():
                          (f"poly/mont/{c}_poly_mont.h", r"ntt_(forward|inverse)\(|_by_vanishing\s*\("),
                          (f"array/mont/{c}_arr_mont.h", r"_arr_mont_\w+\s*\("),
                          (f"g1/proj/{c}_G1_proj.h", r"_(batch_(from|to)_affine|fft_(forward|inverse))\s*\("),
+                         (f"g1/jac/{c}_G1_jac.h", r"_(batch_(from|to)_affine|fft_(forward|inverse))\s*\("),
                          (f"g2/proj/{c}_G2_proj.h", r"MSM_(mont|std)_coeff_(proj|affine)_out\(")):
             for line in open(os.path.join(ref, hdr)):
                 if re.search(pat, line) and "slow_reference" not in line and "noalloc" not in line:

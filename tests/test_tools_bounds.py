@@ -17,13 +17,14 @@ def _load(name):
 def test_lazy_bounds_all_paths():
     """every lazy path (both MSM base fields' mixed and full additions, the group FFT's lazy
     Jacobian doubling and cached addition on both base fields, the NTT butterflies of every radix,
-    the closing reductions, the scalar REDC) satisfies its limb / value bounds"""
+    the closing reductions, the scalar REDC, the round-6 product-free radix conversions of the
+    9 x 29-bit fields) satisfies its limb / value bounds"""
     spec, mod = _load("lazy_bounds")
     spec.loader.exec_module(mod)
     ok, results = mod.run_all(verbose=False)
     assert ok, [r for r in results if r[2] != "ok"]
-    assert len(results) == 14
-    assert {fn for _, fn, _ in results} >= {"jac_dbl_lazy", "jac_add_cached_lazy"}
+    assert len(results) == 17
+    assert {fn for _, fn, _ in results} >= {"jac_dbl_lazy", "jac_add_cached_lazy", "radix_conv"}
 
 
 def test_lazy_jacobian_checker_rejects_a_tight_constant():

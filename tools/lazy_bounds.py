@@ -608,6 +608,27 @@ def jac_add_cached_lazy(F):
     F.log.append(f"{tag}: X3 < {F.units(X3):.1f} p, V - X3 < {F.units(t):.1f} p, Y3 < {F.units(Y3):.2f} p")
 
 
+def radix_conv(F):
+    """zk_field.hpp fe_to_int / fe_to_ref on the 9 x 29-bit fields (round 6: R' = 32 R, so the
+    conversions are a product by 32 / by 1/32 instead of a Montgomery product by a constant):
+      fe_mul32_small: any loaded value < 2^256 (a raw reference word, canonical or not) or any
+        product < 2p, shifted by five bits (< 2^261, top limb < 2^29) -> fe_reduce_small, whose
+        quotient estimate is proven here over the WHOLE 9-limb range v < 2^261 (not only < 64p)
+      fe_div32_small: a < 33p -> (a + k p) / 32 < 2p (k < 32) -> fe_canon"""
+    tag = "radix_conv"
+    F.need(F.N == 9 and F.RB == 29, f"{tag}: derived for 9 x 29 limbs")
+    F.need(F.Rp == 32 * (1 << 256), f"{tag}: R' != 32 R")
+    vmax = 1 << 261
+    F.reduce_small_proof(vmax)
+    F.need(32 * ((1 << 256) - 1) < vmax and 32 * 2 * F.p < vmax, f"{tag}: 32 a exceeds 2^261")
+    # to_ref: a < 33 p (every caller passes < 2p: products, the exact 254-bit bucket forms)
+    amax = 33 * F.p - 1
+    F.need(amax + 31 * F.p < 32 * 2 * F.p, f"{tag}: (a + k p) / 32 not < 2p")
+    F.need(amax + 31 * F.p < (1 << 261) * 2 ** 3, f"{tag}: a + k p overflows the 64-bit limb sums")
+    F.log.append(f"{tag}: to_int over v < 2^261 = {(1 << 261) / F.p:.0f} p (reduce_small q_est in {{q-1, q}}); "
+                 f"to_ref (a + k p)/32 < {(amax + 31 * F.p) / 32 / F.p:.2f} p for a < 33p")
+
+
 def check_bn254():
     F = Field("bn254_fp")
     madd_lazy9(F)
@@ -620,9 +641,10 @@ def run_all(verbose=True):
     ok = True
     results = []
     plans = [("bls12_381_fp", [madd_lazy14, add_lazy, add_exact_on_stored, jac_dbl_lazy, jac_add_cached_lazy]),
-             ("bn254_fp", [madd_lazy9, add_lazy, add_exact_on_stored, jac_dbl_lazy, jac_add_cached_lazy]),
-             ("bls12_381_fr", [ntt_paths, scalar_redc]),
-             ("bn254_fr", [ntt_paths, scalar_redc])]
+             ("bn254_fp", [madd_lazy9, add_lazy, add_exact_on_stored, jac_dbl_lazy, jac_add_cached_lazy,
+                           radix_conv]),
+             ("bls12_381_fr", [ntt_paths, scalar_redc, radix_conv]),
+             ("bn254_fr", [ntt_paths, scalar_redc, radix_conv])]
     for name, fns in plans:
         F = Field(name)
         for fn in fns:

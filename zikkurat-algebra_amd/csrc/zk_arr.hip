@@ -105,6 +105,106 @@ __global__ void __launch_bounds__(256) k_arr_map(ArrArgs g) {
   }
 }
 
+// Round 6: the element-wise ops as one kernel PER OP (the switch above compiles every op's registers
+// into every launch) with the HBM accesses of a wavefront staged through LDS: a wave's 64 elements
+// (2 KiB per array) move as two 1-KiB runs of 16 B per lane -- every load and store instruction one
+// contiguous kilobyte -- and each lane takes its 32-B element from the wave's LDS image.  Each wave
+// owns its LDS slices and only reads what its own lanes wrote (no workgroup barrier: the wave's
+// ds_write / ds_read order is kept by the LDS queue of that wave).  STAGED = 0 keeps per-lane 32-B
+// accesses (A/B: ZK_ARR_STAGE=0).
+template <class F>
+__device__ __forceinline__ void ld_staged(Fe<F> &x, const uint64_t *__restrict__ p, size_t e0, size_t n,
+                                          uint4 *__restrict__ sl, int lane) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(p + e0 * 4);
+  const size_t nc = (n - e0 < 64 ? n - e0 : 64) * 2;  // 16-B chunks of this wave's elements
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  const uint4 c0 = (size_t)lane < nc ? src[lane] : z;
+  const uint4 c1 = (size_t)lane + 64 < nc ? src[lane + 64] : z;
+  sl[lane] = c0;
+  sl[lane + 64] = c1;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint4 a = sl[2 * lane], b = sl[2 * lane + 1];
+  uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  fe_unpack(x, w);
+}
+template <class F>
+__device__ __forceinline__ void st_staged(uint64_t *__restrict__ p, size_t e0, size_t n, const Fe<F> &x,
+                                          uint4 *__restrict__ sl, int lane) {
+  Fe<F> c = x;
+  fe_canon(c);
+  uint32_t w[8];
+  fe_pack(w, c);
+  sl[2 * lane] = make_uint4(w[0], w[1], w[2], w[3]);
+  sl[2 * lane + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint4 *dst = reinterpret_cast<uint4 *>(p + e0 * 4);
+  const size_t nc = (n - e0 < 64 ? n - e0 : 64) * 2;
+  if ((size_t)lane < nc) dst[lane] = sl[lane];
+  if ((size_t)lane + 64 < nc) dst[lane + 64] = sl[lane + 64];
+}
+
+template <class F, int OP, bool STAGED>
+__global__ void __launch_bounds__(256) k_arr_op(ArrArgs g) {
+  Fe<F> kA, kB, cs;
+  if (OP == ARR_SCALE || OP == ARR_AXPY || OP == ARR_AXPBY || OP == ARR_SET_CONST) {
+    Fe<F> t;
+    ld_const(t, g.kA);
+    if (OP == ARR_SET_CONST) kA = t; else fe_to_int(kA, t);
+  }
+  if (OP == ARR_AXPBY) {
+    Fe<F> t;
+    ld_const(t, g.kB);
+    fe_to_int(kB, t);
+  }
+  if (OP == ARR_FROM_STD) ld_const(cs, g.cstd);
+  constexpr bool NA = OP != ARR_SET_CONST;
+  constexpr bool NB = OP == ARR_ADD || OP == ARR_SUB || OP == ARR_SUB_REV || OP == ARR_MUL || OP == ARR_MUL_ADD ||
+                      OP == ARR_MUL_SUB || OP == ARR_AXPY || OP == ARR_AXPBY;
+  constexpr bool NC = OP == ARR_MUL_ADD || OP == ARR_MUL_SUB;
+  // [wave][a, b, c][chunk]; the result reuses slice 0 (read before: a wave's DS ops run in order)
+  constexpr int NS = (NA ? 1 : 0) + (NB ? 1 : 0) + (NC ? 1 : 0) > 0 ? (NA ? 1 : 0) + (NB ? 1 : 0) + (NC ? 1 : 0) : 1;
+  __shared__ uint4 lds[4][STAGED ? NS : 1][128];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t n = (size_t)g.n;
+  for (size_t e0b = (size_t)blockIdx.x * 256; e0b < n; e0b += (size_t)gridDim.x * 256) {
+    const size_t e0 = e0b + (size_t)wave * 64;
+    const size_t i = e0 + lane;
+    if (STAGED && e0 >= n) continue;  // the whole wave is past the end (wave-uniform)
+    if (!STAGED && i >= n) continue;
+    Fe<F> x, y, z, r;
+    auto LD = [&](Fe<F> &v, const uint64_t *p, int k) {
+      if (STAGED) ld_staged(v, p, e0, n, lds[wave][STAGED ? k : 0], lane);
+      else ld(v, p, i);
+    };
+    if (NA) LD(x, g.a, 0);
+    if (NB) LD(y, g.b, NA ? 1 : 0);
+    if (NC) LD(z, g.c, NS - 1);
+    switch (OP) {
+      case ARR_NEG: fe_neg(r, x); break;
+      case ARR_ADD: fe_add(r, x, y); break;
+      case ARR_SUB: fe_sub(r, x, y); break;
+      case ARR_SUB_REV: fe_sub(r, y, x); break;
+      case ARR_SQR: { Fe<F> t; fe_sqr(t, x); fe_to_int(r, t); } break;
+      case ARR_MUL: mul_ref(r, x, y); break;
+      case ARR_MUL_ADD: { Fe<F> t; mul_ref(t, x, y); fe_add(r, t, z); } break;
+      case ARR_MUL_SUB: { Fe<F> t; mul_ref(t, x, y); fe_sub(r, t, z); } break;
+      case ARR_SCALE: fe_mul(r, kA, x); break;
+      case ARR_AXPY: { Fe<F> t; fe_mul(t, kA, x); fe_add(r, t, y); } break;
+      case ARR_AXPBY: { Fe<F> t, u; fe_mul(t, kA, x); fe_mul(u, kB, y); fe_add(r, t, u); } break;
+      case ARR_FROM_STD: fe_mul(r, x, cs); break;
+      case ARR_TO_STD: fe_ref_to_std(r, x); break;
+      case ARR_COPY: r = x; break;
+      default: r = kA; break;  // ARR_SET_CONST
+    }
+    if (STAGED) st_staged(g.tgt, e0, n, r, lds[wave][0], lane);
+    else if (i < n) st(g.tgt, i, r);
+  }
+}
+
 // ---------------------------------------------------------------------------- inversion
 
 // x^e (internal form), e = 256-bit exponent (sliding window, zk_field.hpp fe_pow_sw; the
@@ -409,6 +509,50 @@ struct Stage {
   }
 };
 
+// ZK_ARR_STAGE=0: per-lane 32-B accesses (A/B hook, read once); ZK_ARR_MAP=1: the round-5 single
+// switch kernel k_arr_map
+template <class F>
+static void launch_arr_op(int op, const ArrArgs &g, dim3 grid, hipStream_t st) {
+  static const int stage = [] {
+    const char *e = getenv("ZK_ARR_STAGE");
+    return e ? atoi(e) : 1;
+  }();
+  static const bool legacy = [] {
+    const char *e = getenv("ZK_ARR_MAP");
+    return e && e[0] == '1';
+  }();
+  if (legacy) {
+    hipLaunchKernelGGL(k_arr_map<F>, grid, dim3(256), 0, st, g);
+    ZK_CHECK(hipGetLastError());
+    return;
+  }
+#define ZK_ARR_CASE(OPC)                                                                   \
+  case OPC:                                                                                \
+    if (stage) hipLaunchKernelGGL((k_arr_op<F, OPC, true>), grid, dim3(256), 0, st, g);    \
+    else hipLaunchKernelGGL((k_arr_op<F, OPC, false>), grid, dim3(256), 0, st, g);         \
+    break;
+  switch (op) {
+    ZK_ARR_CASE(ARR_NEG)
+    ZK_ARR_CASE(ARR_ADD)
+    ZK_ARR_CASE(ARR_SUB)
+    ZK_ARR_CASE(ARR_SUB_REV)
+    ZK_ARR_CASE(ARR_SQR)
+    ZK_ARR_CASE(ARR_MUL)
+    ZK_ARR_CASE(ARR_MUL_ADD)
+    ZK_ARR_CASE(ARR_MUL_SUB)
+    ZK_ARR_CASE(ARR_SCALE)
+    ZK_ARR_CASE(ARR_AXPY)
+    ZK_ARR_CASE(ARR_AXPBY)
+    ZK_ARR_CASE(ARR_FROM_STD)
+    ZK_ARR_CASE(ARR_TO_STD)
+    ZK_ARR_CASE(ARR_COPY)
+    ZK_ARR_CASE(ARR_SET_CONST)
+    default: ZK_REQUIRE(false, "arr op: unknown op code");
+  }
+#undef ZK_ARR_CASE
+  ZK_CHECK(hipGetLastError());
+}
+
 template <class Cfg>
 static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64_t *b, const uint64_t *c,
                      const uint64_t *kA, const uint64_t *kB, uint64_t *tgt, bool host_io) {
@@ -459,8 +603,7 @@ static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64
       g.kA = load_u256(kA);
       g.kB = load_u256(kB);
       g.cstd = from_std_const<Cfg>();
-      hipLaunchKernelGGL(k_arr_map<F>, dim3(grid_for(N)), dim3(256), 0, st, g);
-      ZK_CHECK(hipGetLastError());
+      launch_arr_op<F>(op, g, dim3(grid_for(N)), st);
     }
   }
   sg.back(tgt, dt, N);

@@ -34,14 +34,15 @@ int poly_div_g(int curve, int n1, const uint64_t *src, int expo_n, const uint64_
                int nrem, uint64_t *rem, bool host_io) {
   return guard_ret(0, [&] { return zk::poly_div_by_vanishing(curve, n1, src, expo_n, eta, nquot, quot, nrem, rem, host_io); });
 }
-void from_affine_g(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
-  guard([&] { zk::g1_batch_from_affine(curve, n, src, tgt, host_io); });
+void from_affine_g(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io, bool jac = false) {
+  guard([&] { zk::g1_batch_from_affine(curve, n, src, tgt, host_io, jac); });
 }
-void to_affine_g(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
-  guard([&] { zk::g1_batch_to_affine(curve, n, src, tgt, host_io); });
+void to_affine_g(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io, bool jac = false) {
+  guard([&] { zk::g1_batch_to_affine(curve, n, src, tgt, host_io, jac); });
 }
-void fft_g(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse) {
-  guard([&] { zk::g1_fft(curve, m, gen, src, tgt, host_io, inverse); });
+void fft_g(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse,
+           bool jac = false) {
+  guard([&] { zk::g1_fft(curve, m, gen, src, tgt, host_io, inverse, jac); });
 }
 }  // namespace
 
@@ -163,6 +164,19 @@ extern "C" {
   }                                                                                                         \
   ZKG_API void PFX##_G1_proj_fft_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {  \
     fft_g(CID, m, gen, src, tgt, true, true);                                                              \
+  }                                                                                                         \
+  /* Jacobian twins (bls12_381_G1_jac.c:139-158, 727-838; G1/Jac.hs:264-265, 374-389) */                   \
+  ZKG_API void PFX##_G1_jac_batch_from_affine(int N, const uint64_t *src, uint64_t *tgt) {                  \
+    from_affine_g(CID, N, src, tgt, true, true);                                                           \
+  }                                                                                                         \
+  ZKG_API void PFX##_G1_jac_batch_to_affine(int N, const uint64_t *src, uint64_t *tgt) {                    \
+    to_affine_g(CID, N, src, tgt, true, true);                                                             \
+  }                                                                                                         \
+  ZKG_API void PFX##_G1_jac_fft_forward(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {   \
+    fft_g(CID, m, gen, src, tgt, true, false, true);                                                       \
+  }                                                                                                         \
+  ZKG_API void PFX##_G1_jac_fft_inverse(int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt) {   \
+    fft_g(CID, m, gen, src, tgt, true, true, true);                                                        \
   }
 
 ZKG_G1EXT_ENTRIES(bn128, ZKG_BN128)
@@ -174,6 +188,13 @@ ZKG_API void zkg_g1_fft_device(int curve, int inverse, int m, const uint64_t *ge
 }
 ZKG_API void zkg_g1_batch_to_affine_device(int curve, int n, const uint64_t *d_src, uint64_t *d_tgt) {
   to_affine_g(curve, n, d_src, d_tgt, false);
+}
+ZKG_API void zkg_g1_jac_fft_device(int curve, int inverse, int m, const uint64_t *gen, const uint64_t *d_src,
+                                   uint64_t *d_tgt) {
+  fft_g(curve, m, gen, d_src, d_tgt, false, inverse != 0, true);
+}
+ZKG_API void zkg_g1_jac_batch_to_affine_device(int curve, int n, const uint64_t *d_src, uint64_t *d_tgt) {
+  to_affine_g(curve, n, d_src, d_tgt, false, true);
 }
 
 }  // extern "C"

@@ -135,8 +135,11 @@ int sharded_msm(int n, const uint64_t *d_expos, int nl, bool mont, const uint64_
       msm_g1<C>((int)(hi - lo), d_expos + lo * nl, nl, d_grps + lo * 2 * NP, /*host_inputs=*/false, mont, window,
                 mine.data() + (size_t)k * 3 * NP);
     }
-  } catch (const Error &e) {
-    local_err = e.what();
+  } catch (const std::exception &e) {  // zk::Error, and std::bad_alloc etc. from the host side: every
+    local_err = e.what();               // rank still joins the all-gather
+    mine[per - 1] = 1;
+  } catch (...) {
+    local_err = "zkg_g1_msm_device_sharded: unknown exception in the chunk MSM";
     mine[per - 1] = 1;
   }
   if (int e = allgather_host(mine.data(), all.data(), per * 8)) return e;

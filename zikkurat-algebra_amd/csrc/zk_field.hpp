@@ -508,21 +508,65 @@ __device__ __forceinline__ void fe_reduce(Fe<F> &a) {
 
 // ---------------------------------------------------------------------------- radix conversion
 
+// Round 6: on the 9 x 29-bit fields R' = 2^261 = 32 R, so the radix conversions are a product by
+// 32 or by 1/32 mod p -- no full Montgomery product (162 mads + bookkeeping) is needed:
+//   to_int  x R -> x R' = 32 (x R):  five-bit limb shift (value < 64p < 2^261 for inputs < 2p),
+//                                    then fe_reduce_small (q estimated from the top limb) -> < 2p;
+//   to_ref  x R' -> x R = (x R' + k p) / 32 with k = -(x R') p^-1 mod 32 (the low five bits of one
+//                                    REDC digit): nine small products and a five-bit shift -> < 1.05p.
+// tools/lazy_bounds.py (radix_conv) checks both on the fields' bounds.
+template <class F>
+__device__ __forceinline__ void fe_mul32_small(Fe<F> &r, const Fe<F> &a) {  // a < 2p normalised -> 32a mod p, < 2p
+  static_assert(F::N == 9 && F::RB == 29, "9 x 29-bit fields only");
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < F::N - 1; i++) {
+    const uint32_t v = a.v[i];
+    r.v[i] = ((v << 5) & F::MASK) | c;
+    c = v >> (F::RB - 5);
+  }
+  r.v[F::N - 1] = (a.v[F::N - 1] << 5) | c;  // 32a < 64p < 2^261: the top limb stays < 2^29
+  fe_reduce_small(r);
+}
+template <class F>
+__device__ __forceinline__ void fe_div32_small(Fe<F> &r, const Fe<F> &a) {  // a < 2p normalised -> a / 32 mod p, < 1.05p
+  static_assert(F::N == 9 && F::RB == 29, "9 x 29-bit fields only");
+  const uint32_t k = (a.v[0] * F::MINV) & 31u;  // a + k p = 0 mod 32
+  uint64_t t[F::N];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {  // a + k p, normalised to 29-bit limbs (top limb unbounded)
+    const uint64_t v = (uint64_t)a.v[i] + (uint64_t)k * F::p(i) + carry;
+    t[i] = (i < F::N - 1) ? (v & F::MASK) : v;
+    carry = v >> F::RB;
+  }
+#pragma unroll
+  for (int i = 0; i < F::N - 1; i++) r.v[i] = (uint32_t)((t[i] >> 5) | ((t[i + 1] << (F::RB - 5)) & F::MASK));
+  r.v[F::N - 1] = (uint32_t)(t[F::N - 1] >> 5);
+}
 // reference Montgomery (R) -> internal (R'):  x*R  ->  x*R'
 template <class F>
 __device__ __forceinline__ void fe_to_int(Fe<F> &r, const Fe<F> &a) {
-  Fe<F> k;
+  if constexpr (F::N == 9 && F::RB == 29) {
+    fe_mul32_small(r, a);
+  } else {
+    Fe<F> k;
 #pragma unroll
-  for (int i = 0; i < F::N; i++) k.v[i] = F::kin(i);
-  fe_mul(r, a, k);
+    for (int i = 0; i < F::N; i++) k.v[i] = F::kin(i);
+    fe_mul(r, a, k);
+  }
 }
 // internal (R') -> reference Montgomery (R), canonical
 template <class F>
 __device__ __forceinline__ void fe_to_ref(Fe<F> &r, const Fe<F> &a) {
-  Fe<F> k;
+  if constexpr (F::N == 9 && F::RB == 29) {
+    fe_div32_small(r, a);
+  } else {
+    Fe<F> k;
 #pragma unroll
-  for (int i = 0; i < F::N; i++) k.v[i] = F::kout(i);
-  fe_mul(r, a, k);
+    for (int i = 0; i < F::N; i++) k.v[i] = F::kout(i);
+    fe_mul(r, a, k);
+  }
   fe_canon(r);
 }
 // reference Montgomery -> standard integer (the reference's `to_std` = REDC(x, 0),

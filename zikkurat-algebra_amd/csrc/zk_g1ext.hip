@@ -5,6 +5,17 @@
 //        (Haskell batchFromAffine / batchToAffine, G1/Proj.hs:409-430; msmProj, :222-223)
 //   <C>_G1_proj_fft_forward / _fft_inverse            bls12_381_G1_proj.c:679-790
 //        (Haskell forwardFFT / inverseFFT = curveFFT / curveIFFT, G1/Proj.hs:270-294)
+// and their Jacobian twins (round 6), bound by the Jacobian G1 instance (G1/Jac.hs:188-196, 264-265,
+// 374-389; msmJac = msm . batchToAffine, Jac.hs:220):
+//   <C>_G1_jac_batch_from_affine / _batch_to_affine   bls12_381_G1_jac.c:139-158
+//   <C>_G1_jac_fft_forward / _fft_inverse             bls12_381_G1_jac.c:727-838
+// The Jacobian FFT is the projective one's text with jac_add / jac_scl (the same per-level scalars,
+// the same group elements), so both run the same stages; only the load (x = X/Z^2, y = Y/Z^3) and the
+// infinity conventions differ: affine infinity -> (1 : 1 : 0) (jac set_infinity, :183-187), Z = 0 ->
+// all-0xFF (to_affine, :120-125), normalised output infinity (0 : 1 : 0) as the projective normalise
+// (jac normalize, :62-67).  An input row with Z = 0 is infinity (the reference's is_infinity also
+// wants Y^2 = X^3, X, Y != 0, :164-180; rows failing that are not curve points and the reference's
+// add takes them as finite, so they are outside the contract).
 //
 // batch_to_affine: the reference inverts every Z separately (Fp_mont_inv per point,
 // G1_proj.c:133-145); here CHK consecutive points per lane share ONE Fermat inversion
@@ -24,6 +35,10 @@
 // 16-entry table per lane in global scratch (no lane divergence on the digit: every window does
 // one table add).
 // Outputs are normalised (Z = 1, infinity = (0:1:0)) as the reference does (:719, :785).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
 #include "zk_curve.hpp"
 #include "zk_host.hpp"
 #include "zk_msm.hpp"
@@ -66,7 +81,7 @@ __device__ __forceinline__ bool ref_all_ones(const uint64_t *p, int words) {
 
 // ---------------------------------------------------------------------------- batch_from_affine
 
-template <class C>
+template <class C, bool JAC>
 __global__ void __launch_bounds__(256) k_from_affine(int n, const uint64_t *__restrict__ src,
                                                      uint64_t *__restrict__ tgt, W6 one_ref) {
   constexpr int NP = C::NP64;
@@ -74,8 +89,9 @@ __global__ void __launch_bounds__(256) k_from_affine(int n, const uint64_t *__re
   if (i >= (size_t)n) return;
   const uint64_t *a = src + i * 2 * NP;
   uint64_t *o = tgt + i * 3 * NP;
-  if (ref_all_ones<typename C::Fp>(a, 2 * NP)) {  // affine infinity -> (0 : 1 : 0), G1_proj.c:121-129
-    for (int k = 0; k < NP; k++) { o[k] = 0; o[NP + k] = one_ref.w[k]; o[2 * NP + k] = 0; }
+  if (ref_all_ones<typename C::Fp>(a, 2 * NP)) {  // affine infinity -> (0 : 1 : 0), G1_proj.c:121-129;
+    // Jacobian: (1 : 1 : 0), G1_jac.c:108-116, 183-187
+    for (int k = 0; k < NP; k++) { o[k] = JAC ? one_ref.w[k] : 0; o[NP + k] = one_ref.w[k]; o[2 * NP + k] = 0; }
   } else {
     for (int k = 0; k < 2 * NP; k++) o[k] = a[k];
     for (int k = 0; k < NP; k++) o[2 * NP + k] = one_ref.w[k];
@@ -86,7 +102,8 @@ __global__ void __launch_bounds__(256) k_from_affine(int n, const uint64_t *__re
 // MODE_PROJ_TO_AFF : src = reference projective (X:Y:Z), tgt = affine (X/Z, Y/Z) / 0xFF..
 // MODE_XYZZ_TO_PROJ: src = device XYZZ, tgt = normalised reference projective, written at
 //                    index bitrev_m(i) when m >= 0 (inverse FFT output order)
-enum { MODE_PROJ_TO_AFF = 0, MODE_XYZZ_TO_PROJ = 1 };
+// MODE_JAC_TO_AFF  : src = reference Jacobian (X:Y:Z), tgt = affine (X/Z^2, Y/Z^3) / 0xFF..
+enum { MODE_PROJ_TO_AFF = 0, MODE_XYZZ_TO_PROJ = 1, MODE_JAC_TO_AFF = 2 };
 
 template <class C, int MODE>
 __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void *__restrict__ srcv,
@@ -101,7 +118,7 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
   const uint64_t *srcp = reinterpret_cast<const uint64_t *>(srcv);
   const uint32_t *srcx = reinterpret_cast<const uint32_t *>(srcv);
   auto den = [&](size_t i, Fe<F> &d) -> bool {  // denominator (internal); false = infinity
-    if (MODE == MODE_PROJ_TO_AFF) {
+    if (MODE != MODE_XYZZ_TO_PROJ) {
       ld_int(d, srcp + i * 3 * NP + 2 * NP);
     } else {
       fe_load_u(d, srcx + i * xw<F>() + 3 * F::SN);  // ZZZ
@@ -129,7 +146,7 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
     if (MODE == MODE_XYZZ_TO_PROJ && bitrev_m > 0)
       o = (size_t)(__builtin_bitreverse32((uint32_t)i) >> (32 - bitrev_m));
     if (!fin) {
-      if (MODE == MODE_PROJ_TO_AFF) {
+      if (MODE != MODE_XYZZ_TO_PROJ) {
         for (int k = 0; k < 2 * NP; k++) tgt[o * 2 * NP + k] = ~0ull;  // G1_proj.c:134-138
       } else {
         uint64_t *q = tgt + o * 3 * NP;
@@ -152,6 +169,16 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
       fe_mul(y, Y, dinv);
       st_ref(tgt + o * 2 * NP, x);
       st_ref(tgt + o * 2 * NP + NP, y);
+    } else if (MODE == MODE_JAC_TO_AFF) {
+      Fe<F> X, Y, x, y, d2, d3;
+      ld_int(X, srcp + i * 3 * NP);
+      ld_int(Y, srcp + i * 3 * NP + NP);
+      fe_sqr(d2, dinv);
+      fe_mul(d3, d2, dinv);
+      fe_mul(x, X, d2);
+      fe_mul(y, Y, d3);
+      st_ref(tgt + o * 2 * NP, x);
+      st_ref(tgt + o * 2 * NP + NP, y);
     } else {
       Xyzz<F> p;
       xyzz_load(p, srcx + i * xw<F>());
@@ -171,8 +198,9 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
 // ---------------------------------------------------------------------------- group FFT
 
 // reference projective -> device XYZZ (x = X/Z -> X' = X Z, ZZ = Z^2; y = Y/Z -> Y' = Y Z^2,
-// ZZZ = Z^3), stored at bitrev_m(i) when m > 0 (forward FFT input order)
-template <class C>
+// ZZZ = Z^3), stored at bitrev_m(i) when m > 0 (forward FFT input order); Jacobian (x = X/Z^2,
+// y = Y/Z^3) -> X' = X, Y' = Y, ZZ = Z^2, ZZZ = Z^3
+template <class C, bool JAC>
 __global__ void __launch_bounds__(256) k_fft_load(int n, int bitrev_m, const uint64_t *__restrict__ src,
                                                   uint32_t *__restrict__ dst) {
   using F = typename C::Fp;
@@ -189,8 +217,13 @@ __global__ void __launch_bounds__(256) k_fft_load(int n, int bitrev_m, const uin
   } else {
     fe_sqr(p.ZZ, Z);
     fe_mul(p.ZZZ, p.ZZ, Z);
-    fe_mul(p.X, X, Z);
-    fe_mul(p.Y, Y, p.ZZ);
+    if (JAC) {
+      p.X = X;
+      p.Y = Y;
+    } else {
+      fe_mul(p.X, X, Z);
+      fe_mul(p.Y, Y, p.ZZ);
+    }
   }
   const size_t o = bitrev_m > 0 ? (size_t)(__builtin_bitreverse32((uint32_t)i) >> (32 - bitrev_m)) : i;
   xyzz_store(dst + o * xw<F>(), p);
@@ -238,7 +271,9 @@ __device__ __forceinline__ void fft_mul(Fe<F> &r, const Fe<F> &a, const Fe<F> &b
 // Invariant of a Jacobian accumulator / table entry: X < 10p, Y, Z < 2p, normalised limbs (every
 // consumer of X multiplies it: the XYZZ it is converted to keeps X < 10p, which xyzz_add and the
 // normalisation only multiply).  tools/lazy_bounds.py (jac_dbl_lazy, jac_add_cached_lazy) replays
-// both routines on that invariant: outputs X < 9p, Y, Z < 1.02p, every column < 2^64.
+// both routines on that invariant for each field: outputs X < 9p, every column < 2^64, and Y, Z < 1.02p
+// on BLS12-381 (R'/p ~ 2520) but Y < 1.41p, Z < 1.05p on BN254 (R'/p ~ 169: the Y3 pair's larger
+// quotient) -- still inside the < 2p invariant; `python tools/lazy_bounds.py` prints these per field.
 #ifndef ZK_FFT_LAZY
 #define ZK_FFT_LAZY 1
 #endif
@@ -886,6 +921,92 @@ __global__ void __launch_bounds__(256, fft_waves<C>()) k_fft_inv_first_glv(int m
   }
 }
 
+// ---------------------------------------------------------------------------- radix-2^b GLV stages
+// (round 6) At KZG SRS sizes (2^12 - 2^14 points, examples/KZG.hs:55) a radix-2 stage holds N lanes
+// (two per butterfly) = 64 - 256 wavefronts for 1024 SIMDs, and every stage is one lane's ~1250-
+// product chain: the transform costs m chains.  On the order-r subgroup the per-level scalars may be
+// combined mod r, so a stage can take b bits at once: a Stockham radix-r step (r = 2^b, natural
+// order in and out) with the r-point DFT's roots folded into the twiddles.  With L the transform
+// length done so far, L' = r L and G = N / L' classes, the data holds at index c + (N / L) k the
+// length-L DFT of x[c + (N / L) n]; a step computes, for each class c' < G and k0 < L,
+//   X[c' + G (k0 + q L)] = sum_{m < r} w_N^(G m k0 + m q N / r) A[c' + G (m + r k0)],   q < r,
+// whose scalar is w_N^(G m k0 + delta N / r) times (-1)^sigma for m q mod r = delta + sigma r / 2: the
+// products are (m, delta) pairs -- 1 / 5 / 21 / 85 per group for r = 2 / 4 / 8 / 16 -- every one an
+// independent GLV lane pair (k_fft_radix_prod), then each output adds its r terms (k_fft_radix_sum).
+// A stage is then ONE multiplication chain for b bits; the work per point-bit grows (1/2, 5/8, 7/8,
+// 4/3 products), so the planner (radix_plan) takes b > 1 only while the stage's lanes fit about one
+// wavefront per SIMD.  The inverse is the same DIT with w^-1 and N^-1 folded into the first stage's
+// scalars (the m = 0 term becomes a product too).
+struct RadixPlan {
+  int b, D;              // radix 2^b; products per group
+  uint8_t pm[96], pd[96];  // product p -> (m, delta)
+  uint8_t qmap[16][16];  // (q, m) -> product index (255: the unscaled m = 0 input itself)
+  uint8_t qsgn[16][16];  // (q, m) -> negate
+};
+
+template <class C>
+__global__ void __launch_bounds__(256, fft_waves<C>()) k_fft_radix_prod(int m, int lgG, const uint32_t *__restrict__ A,
+                                                         uint32_t *__restrict__ P, const uint64_t *__restrict__ twg,
+                                                         int scaled, W6 beta_ref, uint32_t *__restrict__ scratch,
+                                                         int lanes, RadixPlan plan) {
+  using F = typename C::Fp;
+  const int b = plan.b;
+  const size_t N = (size_t)1 << m, NG = N >> b, G = (size_t)1 << lgG;
+  const size_t nl = 2 * NG * (size_t)plan.D;  // two lanes per product
+  Fe<F> beta, t0;
+  fe_load_ref(t0, beta_ref.w);
+  fe_to_int(beta, t0);
+  uint32_t *tab = scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * scl_tab_words<F>();
+  for (size_t L = (size_t)blockIdx.x * blockDim.x + threadIdx.x; L < nl; L += (size_t)lanes) {
+    const size_t pair = L >> 1;
+    const int q = (int)(L & 1);
+    const size_t pidx = pair >> (m - b), g = pair & (NG - 1);  // product-major: neighbours share (m, delta)
+    const size_t mm = plan.pm[pidx], dl = plan.pd[pidx];
+    const size_t c = g & (G - 1), k0 = g >> lgG;
+    Xyzz<F> v, t;
+    xyzz_load(v, A + (c + G * (mm + (k0 << b))) * xw<F>());
+    size_t e = (G * mm * k0 + dl * NG) & (N - 1);
+    const bool neg = e >= N / 2;
+    e &= N / 2 - 1;
+    if (e == 0 && !scaled) t = v;  // w^0 = 1 (the pair is uniform: both lanes take this branch)
+    else glv_scl_pair(t, v, twg + e * 8, beta, tab);
+    if (neg) {
+      Xyzz<F> nt;
+      xyzz_neg(nt, t);
+      t = nt;
+    }
+    if (q == 0) xyzz_store(P + (pidx * NG + g) * xw<F>(), t);
+  }
+}
+
+template <class C>
+__global__ void __launch_bounds__(256) k_fft_radix_sum(int m, int lgG, const uint32_t *__restrict__ A,
+                                                       const uint32_t *__restrict__ P, uint32_t *__restrict__ B,
+                                                       RadixPlan plan) {
+  using F = typename C::Fp;
+  const int b = plan.b, r = 1 << b;
+  const size_t N = (size_t)1 << m, NG = N >> b, G = (size_t)1 << lgG;
+  const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= N) return;
+  const size_t g = o & (NG - 1);
+  const int q = (int)(o >> (m - b));
+  const size_t c = g & (G - 1), k0 = g >> lgG;
+  Xyzz<F> acc, t;
+  const int p0 = plan.qmap[q][0];
+  if (p0 == 255) xyzz_load(acc, A + (c + G * (k0 << b)) * xw<F>());
+  else xyzz_load(acc, P + ((size_t)p0 * NG + g) * xw<F>());
+  for (int mm = 1; mm < r; mm++) {
+    xyzz_load(t, P + ((size_t)plan.qmap[q][mm] * NG + g) * xw<F>());
+    if (plan.qsgn[q][mm]) {
+      Xyzz<F> nt;
+      xyzz_neg(nt, t);
+      t = nt;
+    }
+    xyzz_add(acc, t);
+  }
+  xyzz_store(B + o * xw<F>(), acc);  // = c' + G (k0 + q L)
+}
+
 // r = [|z|] p for BLS12-381's z = -0xd201000000010000 (bits 63, 62, 60, 57, 48, 16): 63 doublings
 // and 5 additions, the membership test's chain (k_subgroup_check)
 template <class F>
@@ -1063,7 +1184,7 @@ static W6 one_ref() {
 }
 
 template <class C>
-static void batch_from_affine_t(Device &dev, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
+static void batch_from_affine_t(Device &dev, int n, const uint64_t *src, uint64_t *tgt, bool host_io, bool jac) {
   using HF = typename HostOf<C>::Fp;
   constexpr int NP = C::NP64;
   if (n <= 0) return;
@@ -1079,7 +1200,8 @@ static void batch_from_affine_t(Device &dev, int n, const uint64_t *src, uint64_
     ds = a;
     dt = dev.arena.take<uint64_t>(N * 3 * NP);
   }
-  hipLaunchKernelGGL(k_from_affine<C>, dim3(div_up(N, 256)), dim3(256), 0, st, n, ds, dt, one_ref<HF>());
+  if (jac) hipLaunchKernelGGL((k_from_affine<C, true>), dim3(div_up(N, 256)), dim3(256), 0, st, n, ds, dt, one_ref<HF>());
+  else hipLaunchKernelGGL((k_from_affine<C, false>), dim3(div_up(N, 256)), dim3(256), 0, st, n, ds, dt, one_ref<HF>());
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 3 * NP * 8);  // fresh caller arrays: zk_runtime.hpp
   ZK_CHECK(hipStreamSynchronize(st));
@@ -1103,7 +1225,7 @@ static int norm_chk(size_t N) {
 }
 
 template <class C>
-static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
+static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t *tgt, bool host_io, bool jac) {
   using HF = typename HostOf<C>::Fp;
   constexpr int NP = C::NP64;
   if (n <= 0) return;
@@ -1122,16 +1244,105 @@ static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t 
   uint64_t *scratch = dev.arena.take<uint64_t>(N * NP);
   const int chk = norm_chk(N);
   const size_t lanes = (N + chk - 1) / chk;
-  hipLaunchKernelGGL((k_norm_chunks<C, MODE_PROJ_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, chk,
-                     (const void *)ds, scratch, dt, exp_p_minus_2<HF>(), 0);
+  if (jac)
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE_JAC_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, chk,
+                       (const void *)ds, scratch, dt, exp_p_minus_2<HF>(), 0);
+  else
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE_PROJ_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, chk,
+                       (const void *)ds, scratch, dt, exp_p_minus_2<HF>(), 0);
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 2 * NP * 8);
   ZK_CHECK(hipStreamSynchronize(st));
 }
 
+static RadixPlan make_radix_plan(int b, bool scaled) {
+  RadixPlan pl;
+  memset(&pl, 0, sizeof pl);
+  const int r = 1 << b, h = r > 2 ? r / 2 : 1;
+  int idx[16][16];
+  for (auto &row : idx)
+    for (int &x : row) x = -1;
+  pl.b = b;
+  pl.D = 0;
+  auto add = [&](int mm, int dl) {
+    idx[mm][dl] = pl.D;
+    pl.pm[pl.D] = (uint8_t)mm;
+    pl.pd[pl.D] = (uint8_t)dl;
+    pl.D++;
+  };
+  if (scaled) add(0, 0);
+  for (int mm = 1; mm < r; mm++)
+    for (int q = 0; q < r; q++) {
+      const int dl = (mm * q % r) % h;
+      if (idx[mm][dl] < 0) add(mm, dl);
+    }
+  for (int q = 0; q < r; q++)
+    for (int mm = 0; mm < r; mm++) {
+      if (mm == 0) {
+        pl.qmap[q][0] = scaled ? (uint8_t)idx[0][0] : 255;
+        continue;
+      }
+      const int t = mm * q % r;
+      pl.qmap[q][mm] = (uint8_t)idx[mm][t % h];
+      pl.qsgn[q][mm] = (uint8_t)(r > 2 ? t >= h : t == 1);
+    }
+  return pl;
+}
+// products per group of a radix-2^b stage (unscaled): r = 2, 4, 8, 16 -> 1, 5, 21, 85
+static int radix_products(int b) { return make_radix_plan(b, false).D; }
+
+// Bits per stage for a 2^m GLV transform, or {} for the fused radix-2 stages.  A stage costs its
+// multiplication chain times the rounds its wavefronts take: on BLS12-381 (stages at 445-503
+// VGPRs, one wavefront per SIMD) ceil(waves / 1024) chains; on BN254 (two per SIMD) one chain up to
+// 1024 waves and 1.75 per 2048 beyond (measured: a 2^15 radix-4 stage of 1280 waves took 1.75x a
+// 512-wave radix-2 stage, profiles/r06a_fft_radix_ab.txt).  A radix-2^b stage adds its sum kernel,
+// r - 1 XYZZ additions per output (~1/90 chain each) and ~0.02 chain of launches and product
+// traffic.  The fused radix-2 stages cost their rounds only; the radix plan (dynamic programming
+// over b = 1..4) is taken when it is at least 3 % cheaper.  ZK_FFT_RADIX=1 forces the fused stages,
+// 2..4 that radix for every stage (the last one takes the remainder) -- A/B hooks.
+static double stage_rounds(double waves, int waves_per_simd) {
+  if (waves_per_simd <= 1) return std::ceil(waves / 1024.0);
+  return waves <= 1024.0 ? 1.0 : 1.75 * std::ceil(waves / 2048.0);
+}
+static std::vector<int> radix_plan(int m, int waves_per_simd) {
+  static const int forced = [] {
+    const char *e = getenv("ZK_FFT_RADIX");
+    return e ? atoi(e) : 0;
+  }();
+  std::vector<int> bits;
+  if (forced == 1) return bits;
+  if (forced >= 2 && forced <= 4) {
+    int left = m;
+    while (left > 0) {
+      const int b = std::min(forced, left);
+      bits.push_back(b);
+      left -= b;
+    }
+    return bits;
+  }
+  const double N = std::ldexp(1.0, m);
+  const double glanes = std::min(N, 131072.0);  // the fused stages' lanes (grid-strided beyond)
+  const double fused = m * stage_rounds(glanes / 64.0, waves_per_simd) * std::ceil(N / glanes);
+  std::vector<double> best(m + 1, 1e30);
+  std::vector<int> how(m + 1, 0);
+  best[0] = 0;
+  for (int k = 1; k <= m; k++)
+    for (int b = 1; b <= 4 && b <= k; b++) {
+      const double waves = std::ceil(2.0 * radix_products(b) * (N / (1 << b)) / 64.0);
+      const double c = best[k - b] + stage_rounds(waves, waves_per_simd) + ((1 << b) - 1) / 90.0 + 0.02;
+      if (c < best[k]) {
+        best[k] = c;
+        how[k] = b;
+      }
+    }
+  if (!(best[m] < 0.97 * fused)) return bits;
+  for (int k = m; k > 0; k -= how[k]) bits.push_back(how[k]);
+  return bits;  // any order: every stage is the same Stockham step
+}
+
 template <class C>
 static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io,
-                     bool inverse) {
+                     bool inverse, bool jac) {
   using F = typename C::Fp;
   using HF = typename HostOf<C>::Fp;
   using HR = typename HostOf<C>::Fr;
@@ -1153,10 +1364,21 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   // final N^-1 scaling of N points)
   size_t glanes = N < (1u << 17) ? N : (1u << 17);
   glanes = (glanes + 255) & ~(size_t)255;
-  const size_t tlanes = std::max(lanes, glanes);
+  // radix-2^b stages (GLV path only, m > 0)
+  const std::vector<int> rbits = m > 0 ? radix_plan(m, fft_waves<C>()) : std::vector<int>();
+  const bool radix = !rbits.empty();
+  size_t rlanes = 0, pbuf = 0;
+  if (radix)
+    for (int b : rbits) {
+      const size_t np = (size_t)(make_radix_plan(b, true).D) * (N >> b);
+      rlanes = std::max(rlanes, std::min(2 * np, (size_t)1 << 17));
+      pbuf = std::max(pbuf, np);
+    }
+  rlanes = (rlanes + 255) & ~(size_t)255;
+  const size_t tlanes = std::max(std::max(lanes, glanes), rlanes);
   const size_t nbad = div_up(N, 256);
   dev.arena.reserve(N * 3 * NP * 8 * (host_io ? 2 : 0) + 3 * N * xw<F>() * 4 + tlanes * scl_tab_words<F>() * 4 +
-                    tw_cnt * 32 + 2 * tw_cnt * 64 + 64 + nbad * 4 + N * NP * 8 + (1 << 20));
+                    tw_cnt * 32 + 2 * tw_cnt * 64 + 64 + nbad * 4 + N * NP * 8 + pbuf * xw<F>() * 4 + (1 << 20));
   dev.arena.reset();
   const uint64_t *ds = src;
   uint64_t *dt = tgt;
@@ -1173,9 +1395,24 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   uint64_t *twg = dev.arena.take<uint64_t>(2 * tw_cnt * 8 + 8);  // w^e, then (w^-1)^e N^-1, then N^-1
   uint32_t *bad = dev.arena.take<uint32_t>(nbad);
   uint64_t *nscratch = dev.arena.take<uint64_t>(N * NP);
+  uint32_t *Pb = radix ? dev.arena.take<uint32_t>(pbuf * xw<F>()) : nullptr;
 
-  hipLaunchKernelGGL(k_fft_load<C>, dim3(div_up(N, 256)), dim3(256), 0, st, (int)N, inverse ? 0 : m, ds, A);
-  ZK_CHECK(hipGetLastError());
+  // input order: bit-reversed for the radix-2 forward stages, natural for the inverse (DIF) and the
+  // Stockham radix-2^b stages
+  auto load_points = [&](bool natural) {
+    const int br = (inverse || natural) ? 0 : m;
+    if (jac)
+      hipLaunchKernelGGL((k_fft_load<C, true>), dim3(div_up(N, 256)), dim3(256), 0, st, (int)N, br, ds, A);
+    else
+      hipLaunchKernelGGL((k_fft_load<C, false>), dim3(div_up(N, 256)), dim3(256), 0, st, (int)N, br, ds, A);
+    ZK_CHECK(hipGetLastError());
+  };
+  static const bool glv_on0 = [] {
+    const char *e = getenv("ZK_FFT_GLV");
+    return !(e && e[0] == '0');
+  }();
+  const bool use_radix = radix && glv_on0;
+  load_points(use_radix);
   // GLV stages when every point is in the order-r subgroup (always on BN254, cofactor 1; checked
   // on BLS12-381).  ZK_FFT_GLV=0: the integer stages always (A/B hook, read once).
   static const bool glv_on = [] {
@@ -1192,6 +1429,15 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   // read after the stages) discards the GLV result and reruns the integer stages from the input.
   uint32_t *hb = nullptr;
   unsigned cgrid = 0;
+  // Every exit path -- a throw from the stages or the fallback in recoverable error mode included --
+  // waits for the side stream's test and its copy into the pinned staging before this call returns,
+  // so no late copy can land in the next call's staging or arena.
+  struct AuxJoin {
+    hipStream_t s = nullptr;
+    ~AuxJoin() {
+      if (s) (void)hipStreamSynchronize(s);
+    }
+  } aux_join;
   if (glv && C::NP64 == 6) {
     uint32_t *Acopy = dev.arena.take<uint32_t>(N * xw<F>());
     ZK_CHECK(hipMemcpyAsync(Acopy, A, N * xw<F>() * 4, hipMemcpyDeviceToDevice, st));
@@ -1199,6 +1445,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
     ZK_CHECK(hipEventRecord(loaded, st));
     hipStream_t st2 = dev.aux_stream();
     ZK_CHECK(hipStreamWaitEvent(st2, loaded, 0));
+    aux_join.s = st2;
     cgrid = (unsigned)(glanes / 256);
     hipLaunchKernelGGL(k_subgroup_check<C>, dim3(cgrid), dim3(256), 0, st2, (int)N, Acopy, beta, (int)glanes, bad);
     ZK_CHECK(hipGetLastError());
@@ -1206,6 +1453,45 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
     ZK_CHECK(hipMemcpyAsync(hb, bad, cgrid * 4, hipMemcpyDeviceToHost, st2));
     ZK_CHECK(hipEventRecord(checked, st2));
   }
+  // Stockham radix-2^b stages (natural order in and out)
+  auto run_radix = [&] {
+    zkh::Fe<HR> g, one, ninv;
+    memcpy(g.v, gen, sizeof g.v);
+    zkh::set_one(one);
+    if (inverse) zkh::inv(g, g);
+    W6 wb = {{0, 0, 0, 0, 0, 0}}, ws = {{0, 0, 0, 0, 0, 0}}, wn = {{0, 0, 0, 0, 0, 0}};
+    for (int j = 0; j < 4; j++) { wb.w[j] = g.v[j]; ws.w[j] = one.v[j]; }
+    hipLaunchKernelGGL(k_fft_tw_glv<Fr>, dim3(div_up(tw_cnt, 256)), dim3(256), 0, st, (int)tw_cnt, wb, ws, gp, twg);
+    ZK_CHECK(hipGetLastError());
+    uint64_t *twn = twg + tw_cnt * 8;
+    if (inverse) {  // N^-1 folded into the first stage's scalars
+      zkh::Fe<HR> nn = one;
+      for (int k = 0; k < m; k++) zkh::add(nn, nn, nn);
+      zkh::inv(ninv, nn);
+      for (int j = 0; j < 4; j++) wn.w[j] = ninv.v[j];
+      hipLaunchKernelGGL(k_fft_tw_glv<Fr>, dim3(div_up(tw_cnt, 256)), dim3(256), 0, st, (int)tw_cnt, wb, wn, gp, twn);
+      ZK_CHECK(hipGetLastError());
+    }
+    uint32_t *in = A, *out = B;
+    int done = 0;  // log2 L
+    for (size_t i = 0; i < rbits.size(); i++) {
+      const int b = rbits[i];
+      const bool scaled = inverse && i == 0;
+      const RadixPlan pl = make_radix_plan(b, scaled);
+      const int lgG = m - done - b;
+      const size_t np = (size_t)pl.D * (N >> b);
+      size_t pl_lanes = std::min(2 * np, (size_t)1 << 17);
+      pl_lanes = (pl_lanes + 255) & ~(size_t)255;
+      hipLaunchKernelGGL(k_fft_radix_prod<C>, dim3((unsigned)(pl_lanes / 256)), dim3(256), 0, st, m, lgG, in, Pb,
+                         scaled ? twn : twg, scaled ? 1 : 0, beta, scratch, (int)pl_lanes, pl);
+      ZK_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(k_fft_radix_sum<C>, dim3(div_up(N, 256)), dim3(256), 0, st, m, lgG, in, Pb, out, pl);
+      ZK_CHECK(hipGetLastError());
+      std::swap(in, out);
+      done += b;
+    }
+    return in;
+  };
   auto run_glv = [&] {
     // twiddles (decomposed): forward w^e; inverse (w^-1)^e with the 1/2 per level deferred to one
     // multiplication by N^-1 folded into the first stage (on the subgroup the m halvings = N^-1)
@@ -1278,8 +1564,9 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
     }
     return in;
   };
+  bool out_natural = false;
   if (glv) {
-    uint32_t *res = run_glv();
+    uint32_t *res = use_radix ? run_radix() : run_glv();
     if (hb) {  // the speculative membership test's verdict
       const hipEvent_t checked = dev.split_event(1);
       for (;;) {
@@ -1292,10 +1579,10 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
     }
     if (glv) {
       A = res;
+      out_natural = use_radix;
     } else {  // some point lies outside the r-subgroup: the reference's exact integer schedule
       ZK_CHECK(hipStreamSynchronize(st));
-      hipLaunchKernelGGL(k_fft_load<C>, dim3(div_up(N, 256)), dim3(256), 0, st, (int)N, inverse ? 0 : m, ds, A);
-      ZK_CHECK(hipGetLastError());
+      load_points(false);
       A = run_int();
     }
   } else if (m > 0) {
@@ -1305,7 +1592,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   const int chk = norm_chk(N);
   const size_t nl = (N + chk - 1) / chk;
   hipLaunchKernelGGL((k_norm_chunks<C, MODE_XYZZ_TO_PROJ>), dim3(div_up(nl, 256)), dim3(256), 0, st, (int)N,
-                     chk, (const void *)A, nscratch, dt, exp_p_minus_2<HF>(), inverse ? m : 0);
+                     chk, (const void *)A, nscratch, dt, exp_p_minus_2<HF>(), (inverse && !out_natural) ? m : 0);
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 3 * NP * 8);  // fresh caller arrays: zk_runtime.hpp
   ZK_CHECK(hipStreamSynchronize(st));
@@ -1313,23 +1600,24 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
 
 // ---------------------------------------------------------------------------- public
 
-void g1_batch_from_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
+void g1_batch_from_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io, bool jac) {
   Device &dev = current_device();
   std::lock_guard<std::mutex> lock(dev.mu);
-  if (curve == 0) batch_from_affine_t<BN254>(dev, n, src, tgt, host_io);
-  else batch_from_affine_t<BLS381>(dev, n, src, tgt, host_io);
+  if (curve == 0) batch_from_affine_t<BN254>(dev, n, src, tgt, host_io, jac);
+  else batch_from_affine_t<BLS381>(dev, n, src, tgt, host_io, jac);
 }
-void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io) {
+void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io, bool jac) {
   Device &dev = current_device();
   std::lock_guard<std::mutex> lock(dev.mu);
-  if (curve == 0) batch_to_affine_t<BN254>(dev, n, src, tgt, host_io);
-  else batch_to_affine_t<BLS381>(dev, n, src, tgt, host_io);
+  if (curve == 0) batch_to_affine_t<BN254>(dev, n, src, tgt, host_io, jac);
+  else batch_to_affine_t<BLS381>(dev, n, src, tgt, host_io, jac);
 }
-void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse) {
+void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse,
+            bool jac) {
   Device &dev = current_device();
   std::lock_guard<std::mutex> lock(dev.mu);
-  if (curve == 0) g1_fft_t<BN254>(dev, m, gen, src, tgt, host_io, inverse);
-  else g1_fft_t<BLS381>(dev, m, gen, src, tgt, host_io, inverse);
+  if (curve == 0) g1_fft_t<BN254>(dev, m, gen, src, tgt, host_io, inverse, jac);
+  else g1_fft_t<BLS381>(dev, m, gen, src, tgt, host_io, inverse, jac);
 }
 
 }  // namespace zk

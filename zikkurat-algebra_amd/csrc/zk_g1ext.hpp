@@ -5,12 +5,15 @@
 
 namespace zk {
 
-// affine (x || y, all-0xFF = infinity) -> projective (x : y : 1), infinity -> (0 : 1 : 0)
-void g1_batch_from_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io);
-// projective -> affine (X/Z, Y/Z), Z = 0 -> all-0xFF
-void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io);
-// group FFT of 2^m projective points with Fr generator `gen` (host, Montgomery); outputs normalised
-void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse);
+// affine (x || y, all-0xFF = infinity) -> projective (x : y : 1), infinity -> (0 : 1 : 0);
+// jac: Jacobian (x : y : 1), infinity -> (1 : 1 : 0)
+void g1_batch_from_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io, bool jac = false);
+// projective -> affine (X/Z, Y/Z), Z = 0 -> all-0xFF; jac: Jacobian -> (X/Z^2, Y/Z^3)
+void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bool host_io, bool jac = false);
+// group FFT of 2^m projective (jac: Jacobian) points with Fr generator `gen` (host, Montgomery);
+// outputs normalised (x : y : 1), infinity (0 : 1 : 0), in both coordinate systems
+void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse,
+            bool jac = false);
 // 1 when the most recent group FFT ran the GLV stages (test / bench probe)
 inline std::atomic<int> &g1_fft_last_glv() {
   static std::atomic<int> v{0};

@@ -544,7 +544,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 #define ZK_ACCUM_WAVES14 2  // the 381-bit madd (A/B hook: 3 spilled ~56 VGPRs in round 2)
 #endif
 #ifndef ZK_ACCUM_WAVES20
-#define ZK_ACCUM_WAVES20 2  // BN254 G2 (Fp2 over 10-limb Fp)
+#define ZK_ACCUM_WAVES20 2  // BN254 G2: F2<BN_Fp>, 2 x 9 limbs (N = 18, i.e. 14 < N < 28); the macro keeps its old name
 #endif
 template <class F>
 struct AccumOcc {  // minimum waves per SIMD k_accum is compiled for

@@ -1,6 +1,5 @@
 // zk_runtime.cpp -- per-device context: stream, grow-only arena, pinned staging.
 #include "zk_runtime.hpp"
-#include <sys/mman.h>
 #include <atomic>
 #include <chrono>
 #include <map>

@@ -49,8 +49,8 @@ ARR_OPS = ["is_valid", "is_zero", "is_one", "is_equal", "set_zero", "set_one", "
            "Ax_plus_By", "Ax_plus_By_inplace"]
 REFERENCE_SYMBOLS += [f"{c}_arr_mont_{o}" for c in CURVES for o in ARR_OPS] + [
     f"{c}_poly_mont_{k}_by_vanishing" for c in CURVES for k in ("div", "quot")] + [
-    f"{c}_G1_proj_{f}" for c in CURVES for f in ("batch_from_affine", "batch_to_affine", "fft_forward",
-                                                  "fft_inverse")] + [
+    f"{c}_G1_{co}_{f}" for c in CURVES for co in ("proj", "jac")
+    for f in ("batch_from_affine", "batch_to_affine", "fft_forward", "fft_inverse")] + [
     f"{c}_G2_proj_MSM_{k}_coeff_{o}_out" for c in CURVES for k in ("mont", "std") for o in ("proj", "affine")]
 EXTENSION_SYMBOLS = [
     "zkg_version", "zkg_device_count", "zkg_set_device", "zkg_device_malloc", "zkg_device_free",
@@ -58,7 +58,8 @@ EXTENSION_SYMBOLS = [
     "zkg_g1_proj_add", "zkg_g1_proj_normalize", "zkg_g1_proj_to_affine", "zkg_gen_fr", "zkg_gen_g1_points",
     "zkg_fft_generator", "zkg_msm_default_window", "zkg_msm_window", "zkg_timer_enable", "zkg_timer_reset", "zkg_timer_read",
     "zkg_arr_op_device", "zkg_arr_dot_device", "zkg_arr_powers_device",
-    "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device", "zkg_g2_msm_device",
+    "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device",
+    "zkg_g1_jac_fft_device", "zkg_g1_jac_batch_to_affine_device", "zkg_g2_msm_device",
     "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_msm_set_ysum_mode", "zkg_msm_set_ahead_min", "zkg_ntt_set_max_radix", "zkg_ntt_set_table_max",
     "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_g1_fft_last_glv", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
     "zkg_release", "zkg_comm_unique_id", "zkg_comm_init", "zkg_comm_destroy", "zkg_comm_rank", "zkg_comm_world",
@@ -219,6 +220,14 @@ def msm_jac(curve, coeffs, points, std=False):
     return out
 
 
+def msm_jac_points(curve, coeffs, jac_points):
+    """Jac's Curve.msm: msmJac cs gs = msm cs (batchToAffine gs) (G1/Jac.hs:188, 220), with the
+    conversion on the GPU (<C>_G1_jac_batch_to_affine) instead of N serial CPU inversions."""
+    if jac_points.ndim != 2 or jac_points.shape[1] != 3 * NLIMBS_P[curve]:
+        raise ValueError("msm: incompatible array dimensions")
+    return msm_jac(curve, coeffs, batch_to_affine(curve, jac_points, coords="jac"))
+
+
 def msm_proj(curve, coeffs, proj_points):
     """Proj.msmProj cs gs = msm cs (batchToAffine gs) (G1/Proj.hs:222-223)."""
     if proj_points.ndim != 2 or proj_points.shape[1] != 3 * NLIMBS_P[curve]:
@@ -258,42 +267,52 @@ def g1_add(curve, a, b):
     return out
 
 
-def batch_from_affine(curve, aff):
-    """Proj.batchFromAffine (G1/Proj.hs:409-418)"""
+def batch_from_affine(curve, aff, coords="proj"):
+    """Proj.batchFromAffine (G1/Proj.hs:409-418); coords="jac": Jac.batchFromAffine (G1/Jac.hs:374-380),
+    infinity -> (1 : 1 : 0)"""
     aff = np.ascontiguousarray(aff, dtype=np.uint64)
     out = np.zeros((aff.shape[0], 3 * NLIMBS_P[curve]), dtype=np.uint64)
     require_gpu()
-    getattr(load(), f"{curve}_G1_proj_batch_from_affine")(aff.shape[0], _p(aff), _p(out))
+    getattr(load(), f"{curve}_G1_{_coords(coords)}_batch_from_affine")(aff.shape[0], _p(aff), _p(out))
     return out
 
 
-def batch_to_affine(curve, proj):
-    """Proj.batchToAffine (G1/Proj.hs:420-430); infinity -> all-0xFF"""
+def batch_to_affine(curve, proj, coords="proj"):
+    """Proj.batchToAffine (G1/Proj.hs:420-430); coords="jac": Jac.batchToAffine (G1/Jac.hs:382-389);
+    infinity -> all-0xFF"""
     proj = np.ascontiguousarray(proj, dtype=np.uint64)
     out = np.zeros((proj.shape[0], 2 * NLIMBS_P[curve]), dtype=np.uint64)
     require_gpu()
-    getattr(load(), f"{curve}_G1_proj_batch_to_affine")(proj.shape[0], _p(proj), _p(out))
+    getattr(load(), f"{curve}_G1_{_coords(coords)}_batch_to_affine")(proj.shape[0], _p(proj), _p(out))
     return out
 
 
-def _curve_fft(sg, pts, name, msg):
+def _coords(coords):
+    if coords not in ("proj", "jac"):
+        raise ValueError(f"coords must be 'proj' or 'jac', not {coords!r}")
+    return coords
+
+
+def _curve_fft(sg, pts, name, msg, coords):
     pts = np.ascontiguousarray(pts, dtype=np.uint64)
     if pts.ndim != 2 or sg.size != pts.shape[0]:
         raise ValueError(msg)
     require_gpu()
     out = np.zeros_like(pts)
-    getattr(load(), f"{sg.curve}_G1_proj_{name}")(sg.log_size, _p(sg.gen_array()), _p(pts), _p(out))
+    getattr(load(), f"{sg.curve}_G1_{_coords(coords)}_{name}")(sg.log_size, _p(sg.gen_array()), _p(pts), _p(out))
     return out
 
 
-def forward_fft(sg, pts):
-    """Proj.forwardFFT = curveFFT (G1/Proj.hs:270-281): [L_k(tau)] -> [tau^i] points, normalised"""
-    return _curve_fft(sg, pts, "fft_forward", "forwardNTT: subgroup size differs from the array size")
+def forward_fft(sg, pts, coords="proj"):
+    """Proj.forwardFFT = curveFFT (G1/Proj.hs:270-281; Jacobian: G1/Jac.hs:266-276):
+    [L_k(tau)] -> [tau^i] points, normalised"""
+    return _curve_fft(sg, pts, "fft_forward", "forwardNTT: subgroup size differs from the array size", coords)
 
 
-def inverse_fft(sg, pts):
-    """Proj.inverseFFT = curveIFFT (G1/Proj.hs:283-294): [tau^i] -> [L_k(tau)] points, normalised"""
-    return _curve_fft(sg, pts, "fft_inverse", "inverseNTT: subgroup size differs from the array size")
+def inverse_fft(sg, pts, coords="proj"):
+    """Proj.inverseFFT = curveIFFT (G1/Proj.hs:283-294; Jacobian: G1/Jac.hs:278-288):
+    [tau^i] -> [L_k(tau)] points, normalised"""
+    return _curve_fft(sg, pts, "fft_inverse", "inverseNTT: subgroup size differs from the array size", coords)
 
 
 curve_fft = forward_fft

@@ -357,6 +357,11 @@ ZKG_API int zkg_msm_last_groups(void);
 /* 1 when the most recent group FFT (G1 fft / ifft) ran the GLV stages (every input point in the
  * order-r subgroup), 0 when it ran the integer-scalar stages */
 ZKG_API int zkg_g1_fft_last_glv(void);
+/* the GLV-stage plan of a 2^m group FFT (zk_g1ext.hip radix_plan): writes the bits of each
+ * Stockham radix-2^b stage into bits[0..cap) and returns the stage count (0: the fused radix-2
+ * stages, m of them); zkg_g1_fft_radix_products(b) = GLV lane-pair products per group of 2^b points */
+ZKG_API int zkg_g1_fft_plan(int curve, int m, int *bits, int cap);
+ZKG_API int zkg_g1_fft_radix_products(int b);
 /* device bytes of one G1 MSM's working set (the arena it reserves) with its windows split into
  * `groups` passes; window_size <= 0: the default window */
 ZKG_API size_t zkg_msm_workspace_bytes(int curve, int npoints, int expo_nlimbs, int expos_mont, int host_inputs,

@@ -27,6 +27,19 @@ from oracle.oracle import Reference  # noqa: E402
 
 HBM = 8000.0  # GB/s, MI355X_MICROARCH.md
 CURVE = "bls12_381"
+# measured VALU issue ceiling: v_mad_u64_u32 lane-ops/s of the whole chip (profiles/r02_valu_ceiling.json)
+VALU_SLOTS = 3.42e13
+
+
+def isa_slots(key):
+    """issue slots of one hot-loop iteration from the newest profiles/*_isa_<key>.json
+    (tools/isa_profile.sh; per-lane GLV chain totals: tools/fft_isa.py), or None"""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_isa_{key}.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    return (d.get("hot_loop") or {}).get("issue_slots_per_iteration") or d.get("issue_slots_per_chain")
 
 
 def timeit(fn, reps):
@@ -133,11 +146,21 @@ def main():
             sg = zk.get_fft_subgroup(curve, fm)
             ds, dd = zk.DeviceBuffer(proj), zk.DeviceBuffer.empty(proj.nbytes)
             g = sg.gen_array()
-            row = {}
+            chain = isa_slots(f"glv_chain_{curve}")
+            row = {"plan_bits_per_stage": zk.g1_fft_plan(curve, fm) or [1] * fm}
             for name, inv, smuls in (("forward", 0, N // 2 * fm), ("inverse", 1, N * fm)):
                 sec = timeit(lambda: lib.zkg_g1_fft_device(cid, inv, fm, P(g), ds.ptr, dd.ptr), 1 if fm >= 18 else 3)
                 row[name] = {"ms": sec * 1e3, "points_per_s": N / sec, "scalar_muls": smuls,
                              "scalar_muls_per_s": smuls / sec, "glv": bool(zk.g1_fft_last_glv())}
+                if chain and row[name]["glv"]:
+                    pm = zk.g1_fft_glv_products(curve, fm, inverse=bool(inv))
+                    iss = pm * 2 * chain / sec  # two lanes (a GLV pair) per product
+                    row[name]["valu_roofline"] = {
+                        "bound": "valu_issue", "glv_pair_products": pm, "issue_slots_per_lane_chain": chain,
+                        "achieved": iss, "peak": VALU_SLOTS, "unit": "issue slots/s", "frac": iss / VALU_SLOTS,
+                        "note": "scalar-multiplication chains only (additions, loads, sums, normalisation not "
+                                "counted); below 2^15 a stage is latency-bound by construction (fewer lanes than "
+                                "one wavefront per SIMD)"}
             fft[f"{curve}_2^{fm}"] = row
             ds.free()
             dd.free()
@@ -152,26 +175,42 @@ def main():
     out["g1_group_fft"] = fft
 
     # ---------------------------------------------------------------- G2 MSM, both curves
-    from test_gpu_g2 import g2_points
+    # DISTINCT points (verdict r05 item 1): P0 + i H over the reference's own G2 arithmetic
+    # (golden_io.g2_points), so the large-window sort and the Y sums see real bucket occupancy
+    import golden_io
     lib.zkg_g2_msm_device.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     out["g2_msm"] = {}
     for curve in ("bls12_381", "bn128"):
-        uniq = g2_points(ref, curve, 1 << 14) if ref else None
-        if uniq is None:
+        if not ref:
             break
-        for gm in ((16,) if args.quick else (18, 20)):
+        gms = (16,) if args.quick else (18, 20)
+        t0 = time.perf_counter()
+        allpts = golden_io.g2_points(ref.lib, curve, 1 << max(gms))
+        gen_s = time.perf_counter() - t0
+        slots = isa_slots(f"k_accum_{curve}_g2")
+        for gm in gms:
             ng = 1 << gm
-            pts = np.ascontiguousarray(np.resize(uniq, (ng, uniq.shape[1])))
+            pts = np.ascontiguousarray(allpts[:ng])
             sc = zk.gen_fr(curve, 8, ng)
             dsc, dpt = zk.DeviceBuffer(sc), zk.DeviceBuffer(pts)
             res = np.zeros(36, np.uint64)
             sec = timeit(lambda: lib.zkg_g2_msm_device(zk.CURVE_ID[curve], ng, dsc.ptr, 4, 1, dpt.ptr, P(res), 0), 3)
-            g2 = {"n": ng, "ms": sec * 1e3, "pairs_per_s": ng / sec,
-                  "roofline": hbm((32 + 4 * 8 * zk.NLIMBS_P[curve]) * ng, sec),
-                  "note": "VALU bound (Fp2 products), like G1; points: 2^14 distinct reference-generated G2 points "
-                          "repeated"}
-            if gm == (16 if args.quick else 18):
+            c = lib.zkg_msm_default_window(ng)
+            W = (255 if curve == "bls12_381" else 254) // c + 1
+            g2 = {"n": ng, "ms": sec * 1e3, "pairs_per_s": ng / sec, "window": c, "windows": W,
+                  "hbm_fraction": hbm((32 + 4 * 8 * zk.NLIMBS_P[curve]) * ng, sec)["frac"],
+                  "note": f"{ng} distinct reference-generated G2 points (generated in {gen_s:.0f} s on the host)"}
+            if slots:
+                madds = W * ng  # one Fp2 mixed add per (window, pair) in the accumulation
+                iss = madds * slots / sec
+                g2["valu_roofline"] = {"bound": "valu_issue", "madds": madds, "issue_slots_per_madd": slots,
+                                       "achieved": iss, "peak": VALU_SLOTS, "unit": "issue slots/s",
+                                       "frac": iss / VALU_SLOTS,
+                                       "note": "the accumulation's madds x its ISA slot count over the WHOLE "
+                                               "MSM time (sort, Y sums and the tail included): a lower bound "
+                                               "on the accumulation kernel's own issue fraction"}
+            if gm == gms[0]:
                 s_ = 1 << 12
                 w = np.zeros(4 * zk.NLIMBS_P[curve], np.uint64)
                 t = cpu_time(lambda: ref.arr(curve, "G2_proj_MSM_mont_coeff_affine_out", s_, sc[:s_], pts[:s_], w, 4))

@@ -1,7 +1,7 @@
 """G2 MSM timing, device-resident (GPU box; A/B of variant builds via ZK_LIB_PATH):
     python tools/g2_time.py [curve ...]
-2^14 distinct reference-generated G2 points repeated to 2^18 / 2^20 pairs (as tools/bench_ext.py),
-3 reps after a warm-up; prints ms and a digest of the projective result."""
+2^18 / 2^20 DISTINCT reference-generated G2 points (golden_io.g2_points, as tools/bench_ext.py since
+round 6), 3 reps after a warm-up; prints ms and a digest of the projective result."""
 import ctypes
 import hashlib
 import os
@@ -14,7 +14,7 @@ for p in (os.path.join(ROOT, "zikkurat-algebra_amd"), os.path.join(ROOT, "tests"
 import numpy as np  # noqa: E402
 import zkalgebra as zk  # noqa: E402
 from oracle.oracle import Reference  # noqa: E402
-from test_gpu_g2 import g2_points  # noqa: E402
+import golden_io  # noqa: E402
 
 
 def main():
@@ -24,10 +24,10 @@ def main():
                                       ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     ref = Reference()
     for curve in sys.argv[1:] or ("bn128", "bls12_381"):
-        uniq = g2_points(ref, curve, 1 << 14)
+        allpts = golden_io.g2_points(ref.lib, curve, 1 << 20)
         for gm in (18, 20):
             ng = 1 << gm
-            pts = np.ascontiguousarray(np.resize(uniq, (ng, uniq.shape[1])))
+            pts = np.ascontiguousarray(allpts[:ng])
             sc = zk.gen_fr(curve, 8, ng)
             dsc, dpt = zk.DeviceBuffer(sc), zk.DeviceBuffer(pts)
             res = np.zeros(36, np.uint64)

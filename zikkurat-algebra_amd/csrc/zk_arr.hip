@@ -112,14 +112,35 @@ __global__ void __launch_bounds__(256) k_arr_map(ArrArgs g) {
 // owns its LDS slices and only reads what its own lanes wrote (no workgroup barrier: the wave's
 // ds_write / ds_read order is kept by the LDS queue of that wave).  STAGED = 0 keeps per-lane 32-B
 // accesses (A/B: ZK_ARR_STAGE=0).
-template <class F>
+// NT: nontemporal (streaming) HBM loads and stores -- every byte is touched once (measured on the
+// 512 MiB copy shape, tools/microbench/stream_bw.hip: 5.76 -> 6.22 TB/s with 1024 workgroups,
+// profiles/r06c_stream_bw.txt)
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint4 *p) {
+  if (NT) {
+    const v4u_t v = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(uint4 *p, const uint4 &v) {
+  if (NT) {
+    v4u_t w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<v4u_t *>(p));
+  } else {
+    *p = v;
+  }
+}
+template <class F, bool NT>
 __device__ __forceinline__ void ld_staged(Fe<F> &x, const uint64_t *__restrict__ p, size_t e0, size_t n,
                                           uint4 *__restrict__ sl, int lane) {
   const uint4 *src = reinterpret_cast<const uint4 *>(p + e0 * 4);
   const size_t nc = (n - e0 < 64 ? n - e0 : 64) * 2;  // 16-B chunks of this wave's elements
   const uint4 z = make_uint4(0, 0, 0, 0);
-  const uint4 c0 = (size_t)lane < nc ? src[lane] : z;
-  const uint4 c1 = (size_t)lane + 64 < nc ? src[lane + 64] : z;
+  const uint4 c0 = (size_t)lane < nc ? ld16<NT>(src + lane) : z;
+  const uint4 c1 = (size_t)lane + 64 < nc ? ld16<NT>(src + lane + 64) : z;
   sl[lane] = c0;
   sl[lane + 64] = c1;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -129,7 +150,7 @@ __device__ __forceinline__ void ld_staged(Fe<F> &x, const uint64_t *__restrict__
   uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   fe_unpack(x, w);
 }
-template <class F>
+template <class F, bool NT>
 __device__ __forceinline__ void st_staged(uint64_t *__restrict__ p, size_t e0, size_t n, const Fe<F> &x,
                                           uint4 *__restrict__ sl, int lane) {
   Fe<F> c = x;
@@ -143,11 +164,11 @@ __device__ __forceinline__ void st_staged(uint64_t *__restrict__ p, size_t e0, s
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   uint4 *dst = reinterpret_cast<uint4 *>(p + e0 * 4);
   const size_t nc = (n - e0 < 64 ? n - e0 : 64) * 2;
-  if ((size_t)lane < nc) dst[lane] = sl[lane];
-  if ((size_t)lane + 64 < nc) dst[lane + 64] = sl[lane + 64];
+  if ((size_t)lane < nc) st16<NT>(dst + lane, sl[lane]);
+  if ((size_t)lane + 64 < nc) st16<NT>(dst + lane + 64, sl[lane + 64]);
 }
 
-template <class F, int OP, bool STAGED>
+template <class F, int OP, bool STAGED, bool NT>
 __global__ void __launch_bounds__(256) k_arr_op(ArrArgs g) {
   Fe<F> kA, kB, cs;
   if (OP == ARR_SCALE || OP == ARR_AXPY || OP == ARR_AXPBY || OP == ARR_SET_CONST) {
@@ -177,7 +198,7 @@ __global__ void __launch_bounds__(256) k_arr_op(ArrArgs g) {
     if (!STAGED && i >= n) continue;
     Fe<F> x, y, z, r;
     auto LD = [&](Fe<F> &v, const uint64_t *p, int k) {
-      if (STAGED) ld_staged(v, p, e0, n, lds[wave][STAGED ? k : 0], lane);
+      if (STAGED) ld_staged<F, NT>(v, p, e0, n, lds[wave][STAGED ? k : 0], lane);
       else ld(v, p, i);
     };
     if (NA) LD(x, g.a, 0);
@@ -200,7 +221,7 @@ __global__ void __launch_bounds__(256) k_arr_op(ArrArgs g) {
       case ARR_COPY: r = x; break;
       default: r = kA; break;  // ARR_SET_CONST
     }
-    if (STAGED) st_staged(g.tgt, e0, n, r, lds[wave][0], lane);
+    if (STAGED) st_staged<F, NT>(g.tgt, e0, n, r, lds[wave][0], lane);
     else if (i < n) st(g.tgt, i, r);
   }
 }
@@ -330,20 +351,38 @@ __global__ void __launch_bounds__(DOT_THREADS) k_dot(int n, const uint64_t *__re
   }
   if (threadIdx.x == 0) st(part, blockIdx.x, acc);  // canonical, still in the R^2/R' form
 }
+// the block partials' sum: one 256-thread block, each thread adding every 256th partial, then the
+// same LDS tree as k_dot (round 5 summed the 1024 partials on ONE thread: 0.34 ms of a 0.55 ms
+// 2^24 dot product, profiles/r06c_prof)
 template <class F>
-__global__ void k_dot_final(int nparts, const uint64_t *__restrict__ part, uint64_t *__restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ void __launch_bounds__(DOT_THREADS) k_dot_final(int nparts, const uint64_t *__restrict__ part,
+                                                           uint64_t *__restrict__ out) {
+  __shared__ uint32_t lds[DOT_THREADS * F::N];
   Fe<F> acc;
   fe_zero(acc);
-  for (int i = 0; i < nparts; i++) {
+  for (int i = threadIdx.x; i < nparts; i += DOT_THREADS) {
     Fe<F> x, s;
     ld(x, part, i);
     fe_add(s, acc, x);
     acc = s;
   }
-  Fe<F> r;
-  fe_to_int(r, acc);  // x y R^2/R' * R'^2/R / R' = x y R
-  st(out, 0, r);
+  for (int q = 0; q < F::N; q++) lds[threadIdx.x * F::N + q] = acc.v[q];
+  __syncthreads();
+  for (int s = DOT_THREADS / 2; s >= 1; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      Fe<F> o, r;
+      for (int q = 0; q < F::N; q++) o.v[q] = lds[(threadIdx.x + s) * F::N + q];
+      fe_add(r, acc, o);
+      acc = r;
+      for (int q = 0; q < F::N; q++) lds[threadIdx.x * F::N + q] = acc.v[q];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    Fe<F> r;
+    fe_to_int(r, acc);  // x y R^2/R' * R'/R = x y R (the product by 32 on the 9 x 29-bit fields)
+    st(out, 0, r);
+  }
 }
 
 // ---------------------------------------------------------------------------- powers
@@ -381,13 +420,20 @@ __global__ void k_pow_tables(int h, int nlo, int nhi, U256 kA, U256 kB, uint64_t
 template <class F>
 __global__ void __launch_bounds__(256) k_powers(int n, int h, const uint64_t *__restrict__ tlo,
                                                 const uint64_t *__restrict__ thi, uint64_t *__restrict__ tgt) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += stride) {
+  // round 6: the output leaves through the wave's LDS image as 1-KiB nontemporal runs (k_arr_op);
+  // the two tables are small and L2-resident
+  __shared__ uint4 lds[4][128];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t N = (size_t)n;
+  for (size_t e0b = (size_t)blockIdx.x * 256; e0b < N; e0b += (size_t)gridDim.x * 256) {
+    const size_t e0 = e0b + (size_t)wave * 64, i = e0 + lane;
+    if (e0 >= N) continue;  // wave-uniform
     Fe<F> lo, hi, r;
-    ld(lo, tlo, i & ((1u << h) - 1));
-    ld(hi, thi, i >> h);
+    const size_t ii = i < N ? i : N - 1;
+    ld(lo, tlo, ii & ((1u << h) - 1));
+    ld(hi, thi, ii >> h);
     fe_mul(r, hi, lo);  // A B^(j 2^h) R * B^l R' / R'
-    st(tgt, i, r);
+    st_staged<F, true>(tgt, e0, N, r, lds[wave], lane);
   }
 }
 
@@ -509,13 +555,25 @@ struct Stage {
   }
 };
 
-// ZK_ARR_STAGE=0: per-lane 32-B accesses (A/B hook, read once); ZK_ARR_MAP=1: the round-5 single
-// switch kernel k_arr_map
+// ZK_ARR_STAGE: 2 (default) staged + nontemporal, 1 staged, 0 per-lane 32-B accesses; ZK_ARR_MAP=1:
+// the round-5 single switch kernel k_arr_map; ZK_ARR_GRID: workgroups of the grid-stride loop
+// (default 1024 = 4 per CU: 5.4-5.8 TB/s on the streaming shapes where 4096 gave 4.4-4.8,
+// profiles/r06c_stream_bw.txt).  A/B hooks, read once.
+static unsigned stream_grid(size_t n) {
+  static const size_t cap = [] {
+    const char *e = getenv("ZK_ARR_GRID");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (size_t)v : (size_t)1024;
+  }();
+  size_t b = (n + 255) / 256;
+  if (b > cap) b = cap;
+  return (unsigned)(b ? b : 1);
+}
 template <class F>
 static void launch_arr_op(int op, const ArrArgs &g, dim3 grid, hipStream_t st) {
   static const int stage = [] {
     const char *e = getenv("ZK_ARR_STAGE");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   static const bool legacy = [] {
     const char *e = getenv("ZK_ARR_MAP");
@@ -528,8 +586,9 @@ static void launch_arr_op(int op, const ArrArgs &g, dim3 grid, hipStream_t st) {
   }
 #define ZK_ARR_CASE(OPC)                                                                   \
   case OPC:                                                                                \
-    if (stage) hipLaunchKernelGGL((k_arr_op<F, OPC, true>), grid, dim3(256), 0, st, g);    \
-    else hipLaunchKernelGGL((k_arr_op<F, OPC, false>), grid, dim3(256), 0, st, g);         \
+    if (stage == 2) hipLaunchKernelGGL((k_arr_op<F, OPC, true, true>), grid, dim3(256), 0, st, g);        \
+    else if (stage == 1) hipLaunchKernelGGL((k_arr_op<F, OPC, true, false>), grid, dim3(256), 0, st, g);  \
+    else hipLaunchKernelGGL((k_arr_op<F, OPC, false, false>), grid, dim3(256), 0, st, g);                 \
     break;
   switch (op) {
     ZK_ARR_CASE(ARR_NEG)
@@ -603,7 +662,7 @@ static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64
       g.kA = load_u256(kA);
       g.kB = load_u256(kB);
       g.cstd = from_std_const<Cfg>();
-      launch_arr_op<F>(op, g, dim3(grid_for(N)), st);
+      launch_arr_op<F>(op, g, dim3(stream_grid(N)), st);
     }
   }
   sg.back(tgt, dt, N);
@@ -649,7 +708,7 @@ static void arr_dot_t(Device &dev, int n, const uint64_t *a, const uint64_t *b, 
   uint64_t *out = dev.arena.take<uint64_t>(4);
   hipLaunchKernelGGL(k_dot<F>, dim3(blocks), dim3(DOT_THREADS), 0, st, n, da, db, part);
   ZK_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_dot_final<F>, dim3(1), dim3(64), 0, st, (int)blocks, part, out);
+  hipLaunchKernelGGL(k_dot_final<F>, dim3(1), dim3(DOT_THREADS), 0, st, (int)blocks, part, out);
   ZK_CHECK(hipGetLastError());
   uint64_t *h = reinterpret_cast<uint64_t *>(dev.host_staging(32));
   ZK_CHECK(hipMemcpyAsync(h, out, 32, hipMemcpyDeviceToHost, st));
@@ -677,7 +736,7 @@ static void arr_powers_t(Device &dev, int n, const uint64_t *kA, const uint64_t 
   hipLaunchKernelGGL(k_pow_tables<F>, dim3(div_up(nt, 256)), dim3(256), 0, st, h, nlo, nhi, load_u256(kA),
                      load_u256(kB), tlo, thi);
   ZK_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_powers<F>, dim3(grid_for(N)), dim3(256), 0, st, n, h, tlo, thi, dt);
+  hipLaunchKernelGGL(k_powers<F>, dim3(stream_grid(N)), dim3(256), 0, st, n, h, tlo, thi, dt);
   ZK_CHECK(hipGetLastError());
   sg.back(tgt, dt, N);
   ZK_CHECK(hipStreamSynchronize(st));

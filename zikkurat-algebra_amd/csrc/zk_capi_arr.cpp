@@ -47,6 +47,8 @@ void fft_g(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t 
 }  // namespace
 
 ZKG_API int zkg_g1_fft_last_glv(void) { return zk::g1_fft_last_glv().load(); }
+ZKG_API int zkg_g1_fft_plan(int curve, int m, int *bits, int cap) { return zk::g1_fft_plan(curve, m, bits, cap); }
+ZKG_API int zkg_g1_fft_radix_products(int b) { return zk::g1_fft_radix_products(b); }
 
 namespace {
 const uint64_t kZero[4] = {0, 0, 0, 0};

@@ -1612,6 +1612,13 @@ void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bo
   if (curve == 0) batch_to_affine_t<BN254>(dev, n, src, tgt, host_io, jac);
   else batch_to_affine_t<BLS381>(dev, n, src, tgt, host_io, jac);
 }
+int g1_fft_plan(int curve, int m, int *bits, int cap) {
+  if (m <= 0) return 0;
+  const std::vector<int> v = radix_plan(m, curve == 0 ? fft_waves<BN254>() : fft_waves<BLS381>());
+  for (int i = 0; i < (int)v.size() && i < cap; i++) bits[i] = v[i];
+  return (int)v.size();
+}
+int g1_fft_radix_products(int b) { return b >= 1 && b <= 4 ? radix_products(b) : 0; }
 void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse,
             bool jac) {
   Device &dev = current_device();

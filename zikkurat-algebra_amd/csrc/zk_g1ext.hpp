@@ -14,6 +14,10 @@ void g1_batch_to_affine(int curve, int n, const uint64_t *src, uint64_t *tgt, bo
 // outputs normalised (x : y : 1), infinity (0 : 1 : 0), in both coordinate systems
 void g1_fft(int curve, int m, const uint64_t *gen, const uint64_t *src, uint64_t *tgt, bool host_io, bool inverse,
             bool jac = false);
+// GLV-stage plan of a 2^m group FFT: bits per Stockham radix-2^b stage (returns the stage count;
+// 0 = the fused radix-2 stages), and the GLV products per group of a radix-2^b stage
+int g1_fft_plan(int curve, int m, int *bits, int cap);
+int g1_fft_radix_products(int b);
 // 1 when the most recent group FFT ran the GLV stages (test / bench probe)
 inline std::atomic<int> &g1_fft_last_glv() {
   static std::atomic<int> v{0};

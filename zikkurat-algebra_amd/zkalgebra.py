@@ -61,7 +61,7 @@ EXTENSION_SYMBOLS = [
     "zkg_poly_div_by_vanishing_device", "zkg_g1_fft_device", "zkg_g1_batch_to_affine_device",
     "zkg_g1_jac_fft_device", "zkg_g1_jac_batch_to_affine_device", "zkg_g2_msm_device",
     "zkg_msm_profile", "zkg_msm_set_group_limit", "zkg_msm_set_ysum_mode", "zkg_msm_set_ahead_min", "zkg_ntt_set_max_radix", "zkg_ntt_set_table_max",
-    "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_g1_fft_last_glv", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
+    "zkg_arena_set_limit", "zkg_msm_last_groups", "zkg_g1_fft_last_glv", "zkg_g1_fft_plan", "zkg_g1_fft_radix_products", "zkg_msm_workspace_bytes", "zkg_set_devices", "zkg_get_devices",
     "zkg_release", "zkg_comm_unique_id", "zkg_comm_init", "zkg_comm_destroy", "zkg_comm_rank", "zkg_comm_world",
     "zkg_comm_allgather", "zkg_comm_barrier", "zkg_comm_max_f64", "zkg_g1_comm_sum_partials",
     "zkg_g1_msm_device_sharded", "zkg_set_error_mode", "zkg_last_error",
@@ -613,6 +613,31 @@ def arena_set_limit(nbytes):
 
 def msm_last_groups():
     return load().zkg_msm_last_groups()
+
+
+def g1_fft_plan(curve, m):
+    """bits per Stockham radix-2^b GLV stage of a 2^m group FFT ([] = the fused radix-2 stages)"""
+    bits = (ctypes.c_int * 32)()
+    k = load().zkg_g1_fft_plan(CURVE_ID[curve], m, bits, 32)
+    return list(bits[:k])
+
+
+def g1_fft_glv_products(curve, m, inverse=False):
+    """GLV lane-pair scalar multiplications one 2^m group FFT runs on subgroup inputs (the fused
+    radix-2 stages: N/2 per stage, minus the j = 0 butterflies; the inverse's first stage: N; the
+    radix-2^b stages: D_b N / 2^b per stage, the few unit-twiddle products (a copy) included)"""
+    n = 1 << m
+    plan = g1_fft_plan(curve, m)
+    if not plan:
+        per = [n // 2 - (n >> s) for s in range(1, m + 1)]  # the N / 2^s j = 0 butterflies copy
+        if inverse:
+            per[-1] = n  # the first inverse stage (s = m) multiplies both outputs (N^-1 folded in)
+        return sum(per)
+    lib = load()
+    tot = 0
+    for i, b in enumerate(plan):
+        tot += lib.zkg_g1_fft_radix_products(b) * (n >> b) + ((n >> b) if inverse and i == 0 else 0)
+    return tot
 
 
 def g1_fft_last_glv():

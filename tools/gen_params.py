@@ -99,6 +99,17 @@ def unsat_block(name, p):
     arr("KIN", (Ri * Ri * pow(R, -1, p)) % p)   # ref Montgomery -> internal:  mont'(x, KIN)
     arr("KOUT", R % p)                     # internal -> ref Montgomery: mont'(x, KOUT)
     arr("KSTD", (Ri * pow(R, -1, p)) % p)  # ref Montgomery -> standard: mont'(x, KSTD)
+    arr("K3", pow(Ri, 3, p))               # (x R')^-1 * R'^3 / R' = x^-1 R' (zk_inv.hpp: after safegcd)
+    # safegcd (zk_inv.hpp): p in signed 62-bit limbs, p^-1 mod 2^62, the constant batch count
+    # ceil(ceil((49 d + 57) / 17) / 62) of 62 divsteps for a d-bit modulus (Bernstein-Yang, d >= 46)
+    nbits = p.bit_length()
+    L62 = (nbits + 2 + 61) // 62
+    steps = (49 * nbits + 57) // 17 + 1
+    vals = ", ".join("%dll" % ((p >> (62 * i)) & ((1 << 62) - 1)) for i in range(L62))
+    out.append(f"#define ZK_{P}_S62_L {L62}")
+    out.append(f"#define ZK_{P}_S62_P {{ {vals} }}")
+    out.append(f"#define ZK_{P}_S62_PINV 0x{pow(p, -1, 1 << 62):016x}ull")
+    out.append(f"#define ZK_{P}_S62_BATCHES {-(-steps // 62)}")
     return out
 
 

@@ -239,7 +239,7 @@ __device__ __forceinline__ void fe_pow_int(Fe<F> &r, const Fe<F> &x, const U256 
 // running prefix products (internal form, packed) in `scratch`; one Fermat inversion of
 // the chunk product; the backward pass emits 1/x_i (ARR_INV) or a_i / x_i (ARR_DIV, with
 // x = b).  Any zero x raises *zflag (the final kernel then zeroes everything).
-template <class F>
+template <class F, bool SG = true>
 __global__ void __launch_bounds__(256) k_inv_chunks(int op, int n, int CHK, const uint64_t *__restrict__ a,
                                                     const uint64_t *__restrict__ x, uint64_t *__restrict__ scratch,
                                                     uint64_t *tgt, U256 pm2, uint32_t *zflag) {
@@ -261,7 +261,8 @@ __global__ void __launch_bounds__(256) k_inv_chunks(int op, int n, int CHK, cons
   }
   if (zero) atomicOr(zflag, 1u);
   Fe<F> inv;
-  fe_pow_int(inv, P, pm2);  // (prod)^-1, internal form
+  if (SG) fe_inv_sg(inv, P);  // (prod)^-1, internal form: divsteps (zk_inv.hpp), Fermat with ZK_INV_SG=0
+  else fe_pow_int(inv, P, pm2);
   for (size_t i = i1; i-- > i0;) {
     Fe<F> prev, out, v, vi, q;
     if (i > i0) ld(prev, scratch, i - 1); else fe_one(prev);
@@ -646,7 +647,15 @@ static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64
       uint32_t *flag = dev.arena.take<uint32_t>(1);
       ZK_CHECK(hipMemsetAsync(flag, 0, 4, st));
       const size_t lanes = (N + CHK - 1) / CHK;
-      hipLaunchKernelGGL(k_inv_chunks<F>, dim3(div_up(lanes, 256)), dim3(256), 0, st, op, n, CHK, da,
+      static const bool sg = [] {
+        const char *e = getenv("ZK_INV_SG");
+        return !(e && e[0] == '0');
+      }();
+      if (sg)
+        hipLaunchKernelGGL((k_inv_chunks<F, true>), dim3(div_up(lanes, 256)), dim3(256), 0, st, op, n, CHK, da,
+                         op == ARR_DIV ? db : da, scratch, dt, p_minus_2<Cfg>(), flag);
+      else
+        hipLaunchKernelGGL((k_inv_chunks<F, false>), dim3(div_up(lanes, 256)), dim3(256), 0, st, op, n, CHK, da,
                          op == ARR_DIV ? db : da, scratch, dt, p_minus_2<Cfg>(), flag);
       ZK_CHECK(hipGetLastError());
       hipLaunchKernelGGL(k_zero_if_flag, dim3(grid_for(N * 4)), dim3(256), 0, st, n, dt, flag);

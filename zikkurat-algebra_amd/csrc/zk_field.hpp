@@ -25,6 +25,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "zk_inv.hpp"
 #include "zk_params.inc"
 
 namespace zk {
@@ -50,6 +51,13 @@ namespace zk {
       constexpr uint32_t v_[] = PFX##_U_KOUT; return v_[i]; }                           \
     __host__ __device__ static constexpr uint32_t kstd(int i) {                         \
       constexpr uint32_t v_[] = PFX##_U_KSTD; return v_[i]; }                           \
+    __host__ __device__ static constexpr uint32_t k3(int i) {                           \
+      constexpr uint32_t v_[] = PFX##_U_K3; return v_[i]; }                             \
+    static constexpr int S62_L = PFX##_S62_L;           /* safegcd limbs (zk_inv.hpp) */ \
+    static constexpr int S62_NB = PFX##_S62_BATCHES;    /* 62-divstep batches */       \
+    static constexpr uint64_t S62_PINV = PFX##_S62_PINV;                              \
+    __host__ __device__ static constexpr int64_t s62p(int i) {                          \
+      constexpr int64_t v_[] = PFX##_S62_P; return v_[i]; }                           \
   };
 
 ZK_DEFINE_FIELD(BN_Fp, ZK_BN128_FP)
@@ -635,6 +643,35 @@ __device__ __forceinline__ void fe_store_ref(uint64_t *__restrict__ p, const Fe<
   uint4 *q = reinterpret_cast<uint4 *>(p);
 #pragma unroll
   for (int i = 0; i < F::NW / 4; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// Inverse in internal form by safegcd (zk_inv.hpp): a = x R' (any value < 2p, normalised limbs) ->
+// x^-1 R' (< 2p).  canon(a) = x R' mod p as an integer; b = (x R')^-1 mod p by divsteps; one product
+// by R'^3 gives x^-1 R'.  a = 0 gives 0.  ~18 / 12 batches of 62 divsteps (381- / 255-bit fields)
+// instead of a 489 / 323-product Fermat chain (round 6).
+template <class F>
+__device__ __forceinline__ void fe_inv_sg(Fe<F> &r, const Fe<F> &a) {
+  Fe<F> c = a;
+  fe_canon(c);
+  uint32_t w[F::NW];
+  fe_pack(w, c);
+  uint64_t x[F::N64], y[F::N64];
+#pragma unroll
+  for (int i = 0; i < F::N64; i++) x[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+  int64_t P[F::S62_L];
+#pragma unroll
+  for (int i = 0; i < F::S62_L; i++) P[i] = F::s62p(i);
+  sg_inverse_words<F::S62_L, F::S62_NB>(y, x, F::N64, P, F::S62_PINV);
+#pragma unroll
+  for (int i = 0; i < F::N64; i++) {
+    w[2 * i] = (uint32_t)y[i];
+    w[2 * i + 1] = (uint32_t)(y[i] >> 32);
+  }
+  Fe<F> b, k;
+  fe_unpack(b, w);
+#pragma unroll
+  for (int i = 0; i < F::N; i++) k.v[i] = F::k3(i);
+  fe_mul(r, b, k);
 }
 
 // internal-form storage: SN u32 words (limbs, zero padded), 16-B aligned

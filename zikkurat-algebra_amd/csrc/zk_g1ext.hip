@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(256) k_from_affine(int n, const uint64_t *__re
 // MODE_JAC_TO_AFF  : src = reference Jacobian (X:Y:Z), tgt = affine (X/Z^2, Y/Z^3) / 0xFF..
 enum { MODE_PROJ_TO_AFF = 0, MODE_XYZZ_TO_PROJ = 1, MODE_JAC_TO_AFF = 2 };
 
-template <class C, int MODE>
+template <class C, int MODE, bool SG = true>
 __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void *__restrict__ srcv,
                                                      uint64_t *__restrict__ scratch, uint64_t *__restrict__ tgt,
                                                      W6 pm2, int bitrev_m) {
@@ -136,7 +136,8 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
     fe_store_ref(scratch + i * NP, P);  // running product (internal form, packed)
   }
   Fe<F> inv;
-  fe_pow_words<F, NP>(inv, P, pm2);
+  if (SG) fe_inv_sg(inv, P);  // divsteps (zk_inv.hpp); Fermat with ZK_INV_SG=0
+  else fe_pow_words<F, NP>(inv, P, pm2);
   Fe<F> one_int;
   fe_one(one_int);
   for (size_t i = i1; i-- > i0;) {
@@ -979,32 +980,57 @@ __global__ void __launch_bounds__(256, fft_waves<C>()) k_fft_radix_prod(int m, i
   }
 }
 
+// The r terms of an output are summed by S = min(r, 4) lanes (each adds every S-th term), then the
+// S partial sums are combined across the lanes by shuffles: log2 S + r / S - 1 additions deep
+// instead of r - 1 (radix 16: 5 instead of 15).  S consecutive lanes per output.
+template <class F>
+__device__ __forceinline__ void xyzz_shfl_xor(Xyzz<F> &r, const Xyzz<F> &a, int mask) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++) {
+    r.X.v[i] = (uint32_t)__shfl_xor((int)a.X.v[i], mask);
+    r.Y.v[i] = (uint32_t)__shfl_xor((int)a.Y.v[i], mask);
+    r.ZZ.v[i] = (uint32_t)__shfl_xor((int)a.ZZ.v[i], mask);
+    r.ZZZ.v[i] = (uint32_t)__shfl_xor((int)a.ZZZ.v[i], mask);
+  }
+}
 template <class C>
 __global__ void __launch_bounds__(256) k_fft_radix_sum(int m, int lgG, const uint32_t *__restrict__ A,
                                                        const uint32_t *__restrict__ P, uint32_t *__restrict__ B,
                                                        RadixPlan plan) {
   using F = typename C::Fp;
   const int b = plan.b, r = 1 << b;
+  const int lgS = b < 2 ? b : 2, S = 1 << lgS;
   const size_t N = (size_t)1 << m, NG = N >> b, G = (size_t)1 << lgG;
-  const size_t o = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= N) return;
+  const size_t gt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t o = gt >> lgS;
+  const int j = (int)(gt & (S - 1));
+  if (o >= N) return;  // N S is a multiple of 64 (N >= 16) or the grid's lanes of one output stay together
   const size_t g = o & (NG - 1);
   const int q = (int)(o >> (m - b));
   const size_t c = g & (G - 1), k0 = g >> lgG;
   Xyzz<F> acc, t;
-  const int p0 = plan.qmap[q][0];
-  if (p0 == 255) xyzz_load(acc, A + (c + G * (k0 << b)) * xw<F>());
-  else xyzz_load(acc, P + ((size_t)p0 * NG + g) * xw<F>());
-  for (int mm = 1; mm < r; mm++) {
-    xyzz_load(t, P + ((size_t)plan.qmap[q][mm] * NG + g) * xw<F>());
-    if (plan.qsgn[q][mm]) {
-      Xyzz<F> nt;
-      xyzz_neg(nt, t);
-      t = nt;
+  xyzz_set_inf(acc);
+  for (int mm = j; mm < r; mm += S) {
+    if (mm == 0) {
+      const int p0 = plan.qmap[q][0];
+      if (p0 == 255) xyzz_load(t, A + (c + G * (k0 << b)) * xw<F>());
+      else xyzz_load(t, P + ((size_t)p0 * NG + g) * xw<F>());
+    } else {
+      xyzz_load(t, P + ((size_t)plan.qmap[q][mm] * NG + g) * xw<F>());
+      if (plan.qsgn[q][mm]) {
+        Xyzz<F> nt;
+        xyzz_neg(nt, t);
+        t = nt;
+      }
     }
     xyzz_add(acc, t);
   }
-  xyzz_store(B + o * xw<F>(), acc);  // = c' + G (k0 + q L)
+  for (int d = 1; d < S; d <<= 1) {
+    Xyzz<F> other;
+    xyzz_shfl_xor(other, acc, d);
+    xyzz_add(acc, other);
+  }
+  if (j == 0) xyzz_store(B + o * xw<F>(), acc);  // = c' + G (k0 + q L)
 }
 
 // r = [|z|] p for BLS12-381's z = -0xd201000000010000 (bits 63, 62, 60, 57, 48, 16): 63 doublings
@@ -1214,6 +1240,23 @@ static void batch_from_affine_t(Device &dev, int n, const uint64_t *src, uint64_
 // (default 65536) within [2, 32] -- 2^16 points: 2 (the group FFT), 2^20: 16.  Measured
 // (profiles/r05u_inversion_chunks.txt): 2^20 0.95 ms at 32, 0.81 at 16, 1.16 at 8; 2^16 0.541 at
 // 4, 0.528 at 2, 0.553 at 1.
+// ZK_INV_SG=0: Fermat inversions in k_norm_chunks (A/B hook, read once; default: safegcd)
+static bool inv_sg() {
+  static const bool on = [] {
+    const char *e = getenv("ZK_INV_SG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+template <class C, int MODE>
+static void launch_norm(dim3 grid, hipStream_t st, int n, int chk, const void *src, uint64_t *scratch, uint64_t *tgt,
+                        W6 pm2, int bitrev_m) {
+  if (inv_sg())
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2, bitrev_m);
+  else
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2, bitrev_m);
+  ZK_CHECK(hipGetLastError());
+}
 static int norm_chk(size_t N) {
   static const size_t target = [] {
     const char *e = getenv("ZK_NORM_LANES");
@@ -1245,11 +1288,9 @@ static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t 
   const int chk = norm_chk(N);
   const size_t lanes = (N + chk - 1) / chk;
   if (jac)
-    hipLaunchKernelGGL((k_norm_chunks<C, MODE_JAC_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, chk,
-                       (const void *)ds, scratch, dt, exp_p_minus_2<HF>(), 0);
+    launch_norm<C, MODE_JAC_TO_AFF>(dim3(div_up(lanes, 256)), st, n, chk, ds, scratch, dt, exp_p_minus_2<HF>(), 0);
   else
-    hipLaunchKernelGGL((k_norm_chunks<C, MODE_PROJ_TO_AFF>), dim3(div_up(lanes, 256)), dim3(256), 0, st, n, chk,
-                       (const void *)ds, scratch, dt, exp_p_minus_2<HF>(), 0);
+    launch_norm<C, MODE_PROJ_TO_AFF>(dim3(div_up(lanes, 256)), st, n, chk, ds, scratch, dt, exp_p_minus_2<HF>(), 0);
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 2 * NP * 8);
   ZK_CHECK(hipStreamSynchronize(st));
@@ -1485,7 +1526,8 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
       hipLaunchKernelGGL(k_fft_radix_prod<C>, dim3((unsigned)(pl_lanes / 256)), dim3(256), 0, st, m, lgG, in, Pb,
                          scaled ? twn : twg, scaled ? 1 : 0, beta, scratch, (int)pl_lanes, pl);
       ZK_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(k_fft_radix_sum<C>, dim3(div_up(N, 256)), dim3(256), 0, st, m, lgG, in, Pb, out, pl);
+      const size_t slanes = N << (b < 2 ? b : 2);
+      hipLaunchKernelGGL(k_fft_radix_sum<C>, dim3(div_up(slanes, 256)), dim3(256), 0, st, m, lgG, in, Pb, out, pl);
       ZK_CHECK(hipGetLastError());
       std::swap(in, out);
       done += b;
@@ -1591,8 +1633,8 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   g1_fft_last_glv().store(glv ? 1 : 0);
   const int chk = norm_chk(N);
   const size_t nl = (N + chk - 1) / chk;
-  hipLaunchKernelGGL((k_norm_chunks<C, MODE_XYZZ_TO_PROJ>), dim3(div_up(nl, 256)), dim3(256), 0, st, (int)N,
-                     chk, (const void *)A, nscratch, dt, exp_p_minus_2<HF>(), (inverse && !out_natural) ? m : 0);
+  launch_norm<C, MODE_XYZZ_TO_PROJ>(dim3(div_up(nl, 256)), st, (int)N, chk, A, nscratch, dt, exp_p_minus_2<HF>(),
+                                    (inverse && !out_natural) ? m : 0);
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 3 * NP * 8);  // fresh caller arrays: zk_runtime.hpp
   ZK_CHECK(hipStreamSynchronize(st));

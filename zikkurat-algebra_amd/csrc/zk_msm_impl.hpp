@@ -1199,8 +1199,8 @@ __global__ void __launch_bounds__(256, ZK_YSUM_WAVES) k_ysum2(const uint32_t *__
 //      LDS per block at BLS12-381: two blocks per CU.  G1 only.  (At BLS12-381 2^20 there are
 //      65536 Y-sum lanes, one wave per SIMD in total, so this shape would only halve the lanes'
 //      work and add fold levels: measured 0.36-0.39 vs 0.32 ms there, profiles/r03i_*.)
-template <class C>
-__global__ void __launch_bounds__(256, 2) k_ysum3(const uint32_t *__restrict__ buckets,
+template <class C, int WAVES = 2>
+__global__ void __launch_bounds__(256, WAVES) k_ysum3(const uint32_t *__restrict__ buckets,
                                                   const uint32_t *__restrict__ offsets,
                                                   const uint8_t *__restrict__ filled, int W, int c, int l0,
                                                   SegRegion r0, SegRegion r1, uint32_t *__restrict__ Y) {
@@ -1537,6 +1537,15 @@ inline std::atomic<int> &ysum_mode() {
     return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }()};
   return v;
+}
+// G2 Y sums through k_ysum3<C, 1> (LDS prefetch) instead of k_ysum2 (register prefetch):
+// ZK_YSUM_G2_LDS=1 / 0 (A/B hook, read once)
+inline bool ysum_g2_lds() {
+  static const bool on = [] {
+    const char *e = getenv("ZK_YSUM_G2_LDS");
+    return e && e[0] == '1';
+  }();
+  return on;
 }
 inline bool ysum3_on(size_t lanes) {
   static const size_t min_lanes = [] {
@@ -2008,6 +2017,13 @@ struct GroupPass {
         if (two_waves)
           hipLaunchKernelGGL((k_ysum3<C>), dim3(nblk), dim3(256), 0, st, buckets, offsets, (const uint8_t *)filled,
                              s.W, c, s.l0, s.r0, s.r1, Y);
+      } else if (ysum_g2_lds()) {
+        // Fp2 (round 6, A/B): the LDS-gather form at one wave per SIMD -- the register prefetch of
+        // k_ysum2 holds a whole Fp2 XYZZ bucket (112 / 72 VGPRs), and BLS12-381's k_ysum2 spills
+        // 247 VGPRs to scratch at 512 + 256 AGPRs; the LDS image is 128 / 80 KB per block
+        two_waves = true;
+        hipLaunchKernelGGL((k_ysum3<C, 1>), dim3(nblk), dim3(256), 0, st, buckets, offsets, (const uint8_t *)filled,
+                           s.W, c, s.l0, s.r0, s.r1, Y);
       }
       if (!two_waves)
         hipLaunchKernelGGL((k_ysum2<C, is_base_field<F>() ? ZK_YSUM_PF != 0 : ZK_YSUM_PF_G2 != 0>), dim3(nblk),

@@ -431,6 +431,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         result["msm_sizes"] = bench_msm_sizes(zk)
         result["group_fft"] = bench_group_fft(zk)
+        result["group_fft_kzg"] = bench_group_fft(zk, m=12, reps=5)  # KZG SRS size (examples/KZG.hs:55)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(zk, curve, seed, args.cpu_msm_log, args.cpu_ntt_log)
     if rank == 0:
@@ -494,6 +495,7 @@ def bench_group_fft(zk, m=16, reps=3):
                                       ctypes.c_void_p, ctypes.c_void_p]
     out = {"log_n": m, "reps": reps}
     for curve in ("bls12_381", "bn128"):
+        out[f"{curve}_plan_bits_per_stage"] = zk.g1_fft_plan(curve, m) or [1] * m
         n = 1 << m
         pts = zk.batch_from_affine(curve, zk.gen_points(curve, 0x5A4B0007, n))
         sg = zk.get_fft_subgroup(curve, m)

@@ -239,18 +239,27 @@ __device__ __forceinline__ void fe_pow_int(Fe<F> &r, const Fe<F> &x, const U256 
 // running prefix products (internal form, packed) in `scratch`; one Fermat inversion of
 // the chunk product; the backward pass emits 1/x_i (ARR_INV) or a_i / x_i (ARR_DIV, with
 // x = b).  Any zero x raises *zflag (the final kernel then zeroes everything).
-template <class F, bool SG = true>
+// Round 6: lane t's chunk is the strided set {t, t + T, t + 2T, ...} (T = lanes) instead of the
+// CHK consecutive elements from t CHK: a wavefront's loads and stores then touch 64 consecutive
+// elements (2 KiB) per instruction, where the consecutive chunks put 64 lanes 4 KiB apart (one
+// cache line per lane per access).  The product trick works on any partition.  STRIDED = false
+// keeps the round-5 chunks (ZK_INV_STRIDE=0, A/B).
+template <class F, bool SG = true, bool STRIDED = true>
 __global__ void __launch_bounds__(256) k_inv_chunks(int op, int n, int CHK, const uint64_t *__restrict__ a,
                                                     const uint64_t *__restrict__ x, uint64_t *__restrict__ scratch,
-                                                    uint64_t *tgt, U256 pm2, uint32_t *zflag) {
+                                                    uint64_t *tgt, U256 pm2, uint32_t *zflag, int lanes) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t i0 = t * CHK;
-  if (i0 >= (size_t)n) return;
-  const size_t i1 = min((size_t)n, i0 + CHK);
+  const size_t T = STRIDED ? (size_t)lanes : 1;
+  const size_t i0 = STRIDED ? t : t * CHK;
+  if ((STRIDED && t >= T) || i0 >= (size_t)n) return;
+  // the chunk: i0, i0 + T, ..., cnt elements
+  const size_t left = ((size_t)n - i0 + T - 1) / T;
+  const size_t cnt = left < (size_t)CHK ? left : (size_t)CHK;
   Fe<F> P;
   fe_one(P);
   bool zero = false;
-  for (size_t i = i0; i < i1; i++) {
+  for (size_t k = 0; k < cnt; k++) {
+    const size_t i = i0 + k * T;
     Fe<F> v, vi, q;
     ld(v, x, i);
     zero |= fe_is_zero(v);
@@ -263,9 +272,10 @@ __global__ void __launch_bounds__(256) k_inv_chunks(int op, int n, int CHK, cons
   Fe<F> inv;
   if (SG) fe_inv_sg(inv, P);  // (prod)^-1, internal form: divsteps (zk_inv.hpp), Fermat with ZK_INV_SG=0
   else fe_pow_int(inv, P, pm2);
-  for (size_t i = i1; i-- > i0;) {
+  for (size_t k = cnt; k-- > 0;) {
+    const size_t i = i0 + k * T;
     Fe<F> prev, out, v, vi, q;
-    if (i > i0) ld(prev, scratch, i - 1); else fe_one(prev);
+    if (k > 0) ld(prev, scratch, i - T); else fe_one(prev);
     fe_mul(out, inv, prev);  // 1/x_i (internal)
     ld(v, x, i);
     fe_to_int(vi, v);
@@ -557,18 +567,26 @@ struct Stage {
 };
 
 // ZK_ARR_STAGE: 2 (default) staged + nontemporal, 1 staged, 0 per-lane 32-B accesses; ZK_ARR_MAP=1:
-// the round-5 single switch kernel k_arr_map; ZK_ARR_GRID: workgroups of the grid-stride loop
-// (default 1024 = 4 per CU: 5.4-5.8 TB/s on the streaming shapes where 4096 gave 4.4-4.8,
-// profiles/r06c_stream_bw.txt).  A/B hooks, read once.
-static unsigned stream_grid(size_t n) {
-  static const size_t cap = [] {
+// the round-5 single switch kernel k_arr_map.  Grid: the streaming shapes are fastest with one
+// workgroup per 256 elements (no grid-stride loop: add / sub 5.8-6.0 TB/s at 2^24, copy 5.8) or 1024
+// workgroups, and worst at the 4096 the round-5 kernel used (tools/microbench/stream_bw.hip,
+// profiles/r06c_stream_bw.txt); the ops with a product per element overlap it with the streams
+// best at 4096 (scale 4.4 -> 4.8 TB/s, mul 4.8 -> 5.0; profiles/r06e_arr_ab.txt, r06f_arr_grid.txt).
+// ZK_ARR_GRID overrides the cap for every op (A/B hook, read once).
+static unsigned stream_grid(size_t n, bool products = false) {
+  static const size_t cap_env = [] {
     const char *e = getenv("ZK_ARR_GRID");
     const long v = e ? atol(e) : 0;
-    return v > 0 ? (size_t)v : (size_t)1024;
+    return v > 0 ? (size_t)v : (size_t)0;
   }();
+  const size_t cap = cap_env ? cap_env : (products ? (size_t)4096 : (size_t)1 << 30);
   size_t b = (n + 255) / 256;
   if (b > cap) b = cap;
   return (unsigned)(b ? b : 1);
+}
+static bool arr_op_has_product(int op) {
+  return op == ARR_SQR || op == ARR_MUL || op == ARR_SCALE || op == ARR_AXPY || op == ARR_AXPBY ||
+         op == ARR_FROM_STD || op == ARR_TO_STD;
 }
 template <class F>
 static void launch_arr_op(int op, const ArrArgs &g, dim3 grid, hipStream_t st) {
@@ -651,12 +669,19 @@ static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64
         const char *e = getenv("ZK_INV_SG");
         return !(e && e[0] == '0');
       }();
-      if (sg)
-        hipLaunchKernelGGL((k_inv_chunks<F, true>), dim3(div_up(lanes, 256)), dim3(256), 0, st, op, n, CHK, da,
-                         op == ARR_DIV ? db : da, scratch, dt, p_minus_2<Cfg>(), flag);
+      static const bool strided = [] {
+        const char *e = getenv("ZK_INV_STRIDE");
+        return !(e && e[0] == '0');
+      }();
+      const dim3 ig(div_up(lanes, 256)), ib(256);
+      const uint64_t *xs = op == ARR_DIV ? db : da;
+      const U256 pm2 = p_minus_2<Cfg>();
+      if (sg && strided)
+        hipLaunchKernelGGL((k_inv_chunks<F, true, true>), ig, ib, 0, st, op, n, CHK, da, xs, scratch, dt, pm2, flag, (int)lanes);
+      else if (sg)
+        hipLaunchKernelGGL((k_inv_chunks<F, true, false>), ig, ib, 0, st, op, n, CHK, da, xs, scratch, dt, pm2, flag, (int)lanes);
       else
-        hipLaunchKernelGGL((k_inv_chunks<F, false>), dim3(div_up(lanes, 256)), dim3(256), 0, st, op, n, CHK, da,
-                         op == ARR_DIV ? db : da, scratch, dt, p_minus_2<Cfg>(), flag);
+        hipLaunchKernelGGL((k_inv_chunks<F, false, false>), ig, ib, 0, st, op, n, CHK, da, xs, scratch, dt, pm2, flag, (int)lanes);
       ZK_CHECK(hipGetLastError());
       hipLaunchKernelGGL(k_zero_if_flag, dim3(grid_for(N * 4)), dim3(256), 0, st, n, dt, flag);
       ZK_CHECK(hipGetLastError());
@@ -671,7 +696,7 @@ static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64
       g.kA = load_u256(kA);
       g.kB = load_u256(kB);
       g.cstd = from_std_const<Cfg>();
-      launch_arr_op<F>(op, g, dim3(stream_grid(N)), st);
+      launch_arr_op<F>(op, g, dim3(stream_grid(N, arr_op_has_product(op))), st);
     }
   }
   sg.back(tgt, dt, N);
@@ -745,7 +770,7 @@ static void arr_powers_t(Device &dev, int n, const uint64_t *kA, const uint64_t 
   hipLaunchKernelGGL(k_pow_tables<F>, dim3(div_up(nt, 256)), dim3(256), 0, st, h, nlo, nhi, load_u256(kA),
                      load_u256(kB), tlo, thi);
   ZK_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_powers<F>, dim3(stream_grid(N)), dim3(256), 0, st, n, h, tlo, thi, dt);
+  hipLaunchKernelGGL(k_powers<F>, dim3(stream_grid(N, true)), dim3(256), 0, st, n, h, tlo, thi, dt);
   ZK_CHECK(hipGetLastError());
   sg.back(tgt, dt, N);
   ZK_CHECK(hipStreamSynchronize(st));

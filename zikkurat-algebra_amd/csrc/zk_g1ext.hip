@@ -105,16 +105,20 @@ __global__ void __launch_bounds__(256) k_from_affine(int n, const uint64_t *__re
 // MODE_JAC_TO_AFF  : src = reference Jacobian (X:Y:Z), tgt = affine (X/Z^2, Y/Z^3) / 0xFF..
 enum { MODE_PROJ_TO_AFF = 0, MODE_XYZZ_TO_PROJ = 1, MODE_JAC_TO_AFF = 2 };
 
-template <class C, int MODE, bool SG = true>
+// Round 6: the chunk of lane t is the strided set {t, t + T, ...} (T = lanes, as k_inv_chunks):
+// neighbouring lanes touch neighbouring point rows.  STRIDED = false: CHK consecutive points.
+template <class C, int MODE, bool SG = true, bool STRIDED = true>
 __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void *__restrict__ srcv,
                                                      uint64_t *__restrict__ scratch, uint64_t *__restrict__ tgt,
-                                                     W6 pm2, int bitrev_m) {
+                                                     W6 pm2, int bitrev_m, int lanes) {
   using F = typename C::Fp;
   constexpr int NP = C::NP64;
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t i0 = t * CHK;
-  if (i0 >= (size_t)n) return;
-  const size_t i1 = min((size_t)n, i0 + CHK);
+  const size_t T = STRIDED ? (size_t)lanes : 1;
+  const size_t i0 = STRIDED ? t : t * CHK;
+  if ((STRIDED && t >= T) || i0 >= (size_t)n) return;
+  const size_t left = ((size_t)n - i0 + T - 1) / T;
+  const size_t cnt = left < (size_t)CHK ? left : (size_t)CHK;
   const uint64_t *srcp = reinterpret_cast<const uint64_t *>(srcv);
   const uint32_t *srcx = reinterpret_cast<const uint32_t *>(srcv);
   auto den = [&](size_t i, Fe<F> &d) -> bool {  // denominator (internal); false = infinity
@@ -127,7 +131,8 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
   };
   Fe<F> P;
   fe_one(P);
-  for (size_t i = i0; i < i1; i++) {
+  for (size_t k = 0; k < cnt; k++) {
+    const size_t i = i0 + k * T;
     Fe<F> d, q;
     if (den(i, d)) {
       fe_mul(q, P, d);
@@ -140,7 +145,8 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
   else fe_pow_words<F, NP>(inv, P, pm2);
   Fe<F> one_int;
   fe_one(one_int);
-  for (size_t i = i1; i-- > i0;) {
+  for (size_t kk = cnt; kk-- > 0;) {
+    const size_t i = i0 + kk * T;
     Fe<F> d;
     const bool fin = den(i, d);
     size_t o = i;
@@ -158,7 +164,7 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
       continue;
     }
     Fe<F> prev, dinv, q;
-    if (i > i0) fe_load_ref(prev, scratch + (i - 1) * NP); else prev = one_int;
+    if (kk > 0) fe_load_ref(prev, scratch + (i - T) * NP); else prev = one_int;
     fe_mul(dinv, inv, prev);  // 1 / d_i
     fe_mul(q, inv, d);
     inv = q;
@@ -1248,13 +1254,28 @@ static bool inv_sg() {
   }();
   return on;
 }
+// ZK_INV_STRIDE=0: consecutive-point chunks (A/B hook, read once; default strided)
+static bool inv_strided() {
+  static const bool on = [] {
+    const char *e = getenv("ZK_INV_STRIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 template <class C, int MODE>
-static void launch_norm(dim3 grid, hipStream_t st, int n, int chk, const void *src, uint64_t *scratch, uint64_t *tgt,
-                        W6 pm2, int bitrev_m) {
-  if (inv_sg())
-    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2, bitrev_m);
+static void launch_norm(hipStream_t st, int n, int chk, const void *src, uint64_t *scratch, uint64_t *tgt, W6 pm2,
+                        int bitrev_m) {
+  const size_t lanes = ((size_t)n + chk - 1) / chk;
+  const dim3 grid(div_up(lanes, 256));
+  if (inv_sg() && inv_strided())
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true, true>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2,
+                       bitrev_m, (int)lanes);
+  else if (inv_sg())
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2,
+                       bitrev_m, (int)lanes);
   else
-    hipLaunchKernelGGL((k_norm_chunks<C, MODE, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2, bitrev_m);
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, false, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2,
+                       bitrev_m, (int)lanes);
   ZK_CHECK(hipGetLastError());
 }
 static int norm_chk(size_t N) {
@@ -1286,11 +1307,10 @@ static void batch_to_affine_t(Device &dev, int n, const uint64_t *src, uint64_t 
   }
   uint64_t *scratch = dev.arena.take<uint64_t>(N * NP);
   const int chk = norm_chk(N);
-  const size_t lanes = (N + chk - 1) / chk;
   if (jac)
-    launch_norm<C, MODE_JAC_TO_AFF>(dim3(div_up(lanes, 256)), st, n, chk, ds, scratch, dt, exp_p_minus_2<HF>(), 0);
+    launch_norm<C, MODE_JAC_TO_AFF>(st, n, chk, ds, scratch, dt, exp_p_minus_2<HF>(), 0);
   else
-    launch_norm<C, MODE_PROJ_TO_AFF>(dim3(div_up(lanes, 256)), st, n, chk, ds, scratch, dt, exp_p_minus_2<HF>(), 0);
+    launch_norm<C, MODE_PROJ_TO_AFF>(st, n, chk, ds, scratch, dt, exp_p_minus_2<HF>(), 0);
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 2 * NP * 8);
   ZK_CHECK(hipStreamSynchronize(st));
@@ -1632,8 +1652,7 @@ static void g1_fft_t(Device &dev, int m, const uint64_t *gen, const uint64_t *sr
   }
   g1_fft_last_glv().store(glv ? 1 : 0);
   const int chk = norm_chk(N);
-  const size_t nl = (N + chk - 1) / chk;
-  launch_norm<C, MODE_XYZZ_TO_PROJ>(dim3(div_up(nl, 256)), st, (int)N, chk, A, nscratch, dt, exp_p_minus_2<HF>(),
+  launch_norm<C, MODE_XYZZ_TO_PROJ>(st, (int)N, chk, A, nscratch, dt, exp_p_minus_2<HF>(),
                                     (inverse && !out_natural) ? m : 0);
   ZK_CHECK(hipGetLastError());
   if (host_io) copy_to_host(dev, st, tgt, dt, N * 3 * NP * 8);  // fresh caller arrays: zk_runtime.hpp

@@ -1538,14 +1538,17 @@ inline std::atomic<int> &ysum_mode() {
   }()};
   return v;
 }
-// G2 Y sums through k_ysum3<C, 1> (LDS prefetch) instead of k_ysum2 (register prefetch):
-// ZK_YSUM_G2_LDS=1 / 0 (A/B hook, read once)
+// G2 Y sums through k_ysum3<C, 1> (LDS prefetch) instead of k_ysum2 (register prefetch): default on
+// for BLS12-381 G2 only (its k_ysum2 spills 247 VGPRs; 1.211 -> 1.126 ms at 2^20, MSM 12.06 -> 11.99
+// ms; BN254 G2 0.498 -> 0.512 ms, off; profiles/r06f_g2lds*).  ZK_YSUM_G2_LDS=1 / 0 forces either
+// (A/B hook, read once).
+template <class F>
 inline bool ysum_g2_lds() {
-  static const bool on = [] {
+  static const int env = [] {
     const char *e = getenv("ZK_YSUM_G2_LDS");
-    return e && e[0] == '1';
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
-  return on;
+  return env >= 0 ? env == 1 : F::N >= 28;
 }
 inline bool ysum3_on(size_t lanes) {
   static const size_t min_lanes = [] {
@@ -2017,7 +2020,7 @@ struct GroupPass {
         if (two_waves)
           hipLaunchKernelGGL((k_ysum3<C>), dim3(nblk), dim3(256), 0, st, buckets, offsets, (const uint8_t *)filled,
                              s.W, c, s.l0, s.r0, s.r1, Y);
-      } else if (ysum_g2_lds()) {
+      } else if (ysum_g2_lds<F>()) {
         // Fp2 (round 6, A/B): the LDS-gather form at one wave per SIMD -- the register prefetch of
         // k_ysum2 holds a whole Fp2 XYZZ bucket (112 / 72 VGPRs), and BLS12-381's k_ysum2 spills
         // 247 VGPRs to scratch at 512 + 256 AGPRs; the LDS image is 128 / 80 KB per block

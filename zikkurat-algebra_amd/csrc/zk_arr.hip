@@ -168,7 +168,34 @@ __device__ __forceinline__ void st_staged(uint64_t *__restrict__ p, size_t e0, s
   if ((size_t)lane + 64 < nc) st16<NT>(dst + lane + 64, sl[lane + 64]);
 }
 
-template <class F, int OP, bool STAGED, bool NT>
+// the global half of ld_staged: a wave's two 1-KiB runs of one array into registers (issued early,
+// so the loads of the next elements fly while the current ones are computed: PF below)
+struct Runs {
+  uint4 c0, c1;
+};
+template <bool NT>
+__device__ __forceinline__ void fetch_runs(Runs &r, const uint64_t *__restrict__ p, size_t e0, size_t n, int lane) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(p + e0 * 4);
+  const size_t nc = (n - e0 < 64 ? n - e0 : 64) * 2;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  r.c0 = (size_t)lane < nc ? ld16<NT>(src + lane) : z;
+  r.c1 = (size_t)lane + 64 < nc ? ld16<NT>(src + lane + 64) : z;
+}
+template <class F>
+__device__ __forceinline__ void place_runs(Fe<F> &x, const Runs &r, uint4 *__restrict__ sl, int lane) {
+  sl[lane] = r.c0;
+  sl[lane + 64] = r.c1;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint4 a = sl[2 * lane], b = sl[2 * lane + 1];
+  uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  fe_unpack(x, w);
+}
+
+// PF: software-pipelined -- the next grid-stride step's runs are fetched into registers before the
+// current step is computed (8 VGPRs per array)
+template <class F, int OP, bool STAGED, bool NT, bool PF = false>
 __global__ void __launch_bounds__(256) k_arr_op(ArrArgs g) {
   Fe<F> kA, kB, cs;
   if (OP == ARR_SCALE || OP == ARR_AXPY || OP == ARR_AXPBY || OP == ARR_SET_CONST) {
@@ -191,19 +218,7 @@ __global__ void __launch_bounds__(256) k_arr_op(ArrArgs g) {
   __shared__ uint4 lds[4][STAGED ? NS : 1][128];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t n = (size_t)g.n;
-  for (size_t e0b = (size_t)blockIdx.x * 256; e0b < n; e0b += (size_t)gridDim.x * 256) {
-    const size_t e0 = e0b + (size_t)wave * 64;
-    const size_t i = e0 + lane;
-    if (STAGED && e0 >= n) continue;  // the whole wave is past the end (wave-uniform)
-    if (!STAGED && i >= n) continue;
-    Fe<F> x, y, z, r;
-    auto LD = [&](Fe<F> &v, const uint64_t *p, int k) {
-      if (STAGED) ld_staged<F, NT>(v, p, e0, n, lds[wave][STAGED ? k : 0], lane);
-      else ld(v, p, i);
-    };
-    if (NA) LD(x, g.a, 0);
-    if (NB) LD(y, g.b, NA ? 1 : 0);
-    if (NC) LD(z, g.c, NS - 1);
+  auto compute = [&](Fe<F> &r, const Fe<F> &x, const Fe<F> &y, const Fe<F> &z) {
     switch (OP) {
       case ARR_NEG: fe_neg(r, x); break;
       case ARR_ADD: fe_add(r, x, y); break;
@@ -221,6 +236,47 @@ __global__ void __launch_bounds__(256) k_arr_op(ArrArgs g) {
       case ARR_COPY: r = x; break;
       default: r = kA; break;  // ARR_SET_CONST
     }
+  };
+  if constexpr (STAGED && PF) {
+    const size_t step = (size_t)gridDim.x * 256;
+    size_t e0 = (size_t)blockIdx.x * 256 + (size_t)wave * 64;
+    Runs ra, rb, rc;
+    if (e0 < n) {
+      if (NA) fetch_runs<NT>(ra, g.a, e0, n, lane);
+      if (NB) fetch_runs<NT>(rb, g.b, e0, n, lane);
+      if (NC) fetch_runs<NT>(rc, g.c, e0, n, lane);
+    }
+    while (e0 < n) {  // wave-uniform
+      Fe<F> x, y, z, r;
+      if (NA) place_runs(x, ra, lds[wave][0], lane);
+      if (NB) place_runs(y, rb, lds[wave][NA ? 1 : 0], lane);
+      if (NC) place_runs(z, rc, lds[wave][NS - 1], lane);
+      const size_t e1 = e0 + step;
+      if (e1 < n) {
+        if (NA) fetch_runs<NT>(ra, g.a, e1, n, lane);
+        if (NB) fetch_runs<NT>(rb, g.b, e1, n, lane);
+        if (NC) fetch_runs<NT>(rc, g.c, e1, n, lane);
+      }
+      compute(r, x, y, z);
+      st_staged<F, NT>(g.tgt, e0, n, r, lds[wave][0], lane);
+      e0 = e1;
+    }
+    return;
+  }
+  for (size_t e0b = (size_t)blockIdx.x * 256; e0b < n; e0b += (size_t)gridDim.x * 256) {
+    const size_t e0 = e0b + (size_t)wave * 64;
+    const size_t i = e0 + lane;
+    if (STAGED && e0 >= n) continue;  // the whole wave is past the end (wave-uniform)
+    if (!STAGED && i >= n) continue;
+    Fe<F> x, y, z, r;
+    auto LD = [&](Fe<F> &v, const uint64_t *p, int k) {
+      if (STAGED) ld_staged<F, NT>(v, p, e0, n, lds[wave][STAGED ? k : 0], lane);
+      else ld(v, p, i);
+    };
+    if (NA) LD(x, g.a, 0);
+    if (NB) LD(y, g.b, NA ? 1 : 0);
+    if (NC) LD(z, g.c, NS - 1);
+    compute(r, x, y, z);
     if (STAGED) st_staged<F, NT>(g.tgt, e0, n, r, lds[wave][0], lane);
     else if (i < n) st(g.tgt, i, r);
   }
@@ -566,7 +622,8 @@ struct Stage {
   }
 };
 
-// ZK_ARR_STAGE: 2 (default) staged + nontemporal, 1 staged, 0 per-lane 32-B accesses; ZK_ARR_MAP=1:
+// ZK_ARR_STAGE: 2 (default) staged + nontemporal, 4 the same software-pipelined (next step's loads
+// issued before the current step's products), 1 staged, 0 per-lane 32-B accesses; ZK_ARR_MAP=1:
 // the round-5 single switch kernel k_arr_map.  Grid: the streaming shapes are fastest with one
 // workgroup per 256 elements (no grid-stride loop: add / sub 5.8-6.0 TB/s at 2^24, copy 5.8) or 1024
 // workgroups, and worst at the 4096 the round-5 kernel used (tools/microbench/stream_bw.hip,
@@ -605,7 +662,8 @@ static void launch_arr_op(int op, const ArrArgs &g, dim3 grid, hipStream_t st) {
   }
 #define ZK_ARR_CASE(OPC)                                                                   \
   case OPC:                                                                                \
-    if (stage == 2) hipLaunchKernelGGL((k_arr_op<F, OPC, true, true>), grid, dim3(256), 0, st, g);        \
+    if (stage == 4) hipLaunchKernelGGL((k_arr_op<F, OPC, true, true, true>), grid, dim3(256), 0, st, g);  \
+    else if (stage == 2) hipLaunchKernelGGL((k_arr_op<F, OPC, true, true>), grid, dim3(256), 0, st, g);   \
     else if (stage == 1) hipLaunchKernelGGL((k_arr_op<F, OPC, true, false>), grid, dim3(256), 0, st, g);  \
     else hipLaunchKernelGGL((k_arr_op<F, OPC, false, false>), grid, dim3(256), 0, st, g);                 \
     break;

@@ -622,13 +622,17 @@ struct Stage {
   }
 };
 
-// ZK_ARR_STAGE: 2 (default) staged + nontemporal, 4 the same software-pipelined (next step's loads
-// issued before the current step's products), 1 staged, 0 per-lane 32-B accesses; ZK_ARR_MAP=1:
-// the round-5 single switch kernel k_arr_map.  Grid: the streaming shapes are fastest with one
-// workgroup per 256 elements (no grid-stride loop: add / sub 5.8-6.0 TB/s at 2^24, copy 5.8) or 1024
-// workgroups, and worst at the 4096 the round-5 kernel used (tools/microbench/stream_bw.hip,
-// profiles/r06c_stream_bw.txt); the ops with a product per element overlap it with the streams
-// best at 4096 (scale 4.4 -> 4.8 TB/s, mul 4.8 -> 5.0; profiles/r06e_arr_ab.txt, r06f_arr_grid.txt).
+// ZK_ARR_STAGE (A/B hook; default: 4 for the streaming ops, 2 for the ops with a product per
+// element): 2 staged + nontemporal, 4 the same software-pipelined (every array's runs fetched before
+// the first is placed; with a grid-stride loop the next step's runs fly during the products), 1
+// staged, 0 per-lane 32-B accesses; ZK_ARR_MAP=1: the round-5 single switch kernel k_arr_map.
+// Grid: the streaming shapes are fastest with one workgroup per 256 elements (no grid-stride loop:
+// add / sub 5.8-6.0 TB/s at 2^24, copy 5.8) or 1024 workgroups, and worst at the 4096 the round-5
+// kernel used (tools/microbench/stream_bw.hip, profiles/r06c_stream_bw.txt); the ops with a product
+// per element overlap it with the streams best at 4096-8192 workgroups (scale 4.4 -> 4.8 TB/s, mul
+// 4.8 -> 5.0-5.2, Ax_plus_y 5.0 -> 5.35 at 8192; profiles/r06e_arr_ab.txt, r06f_arr_grid.txt,
+// r06i_arr_pf_grid.txt).  Stage 4 on the streaming ops: mul_add 5.6 -> 6.0 TB/s, add / sub / copy
+// 5.7-5.9 -> 5.8-6.1 (r06h_arr_pf_ab.txt, r06i); on the product ops it measured level or slower.
 // ZK_ARR_GRID overrides the cap for every op (A/B hook, read once).
 static unsigned stream_grid(size_t n, bool products = false) {
   static const size_t cap_env = [] {
@@ -636,7 +640,7 @@ static unsigned stream_grid(size_t n, bool products = false) {
     const long v = e ? atol(e) : 0;
     return v > 0 ? (size_t)v : (size_t)0;
   }();
-  const size_t cap = cap_env ? cap_env : (products ? (size_t)4096 : (size_t)1 << 30);
+  const size_t cap = cap_env ? cap_env : (products ? (size_t)8192 : (size_t)1 << 30);
   size_t b = (n + 255) / 256;
   if (b > cap) b = cap;
   return (unsigned)(b ? b : 1);
@@ -647,10 +651,11 @@ static bool arr_op_has_product(int op) {
 }
 template <class F>
 static void launch_arr_op(int op, const ArrArgs &g, dim3 grid, hipStream_t st) {
-  static const int stage = [] {
+  static const int stage_env = [] {
     const char *e = getenv("ZK_ARR_STAGE");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : -1;
   }();
+  const int stage = stage_env >= 0 ? stage_env : (arr_op_has_product(op) ? 2 : 4);
   static const bool legacy = [] {
     const char *e = getenv("ZK_ARR_MAP");
     return e && e[0] == '1';

@@ -2427,7 +2427,12 @@ static void msm_run(Device &dev, int n, const ScalarSlice &sc_in, const uint64_t
       pass.ready_sc = ready_sc;
       pass.ready_pt = ready_pt;
       pass.pts_ref = pts_ref;
-      if (NS > 1) pass.sst = dev.aux2_stream();
+      // ZK_MSM_SORT_INLINE=1 (A/B hook, read once): every split's sort on the main stream, in line
+      static const bool sort_inline = [] {
+        const char *e = getenv("ZK_MSM_SORT_INLINE");
+        return e && e[0] == '1';
+      }();
+      if (NS > 1 && !sort_inline) pass.sst = dev.aux2_stream();
     }
     inputs_on_aux = false;
     pass.launch();

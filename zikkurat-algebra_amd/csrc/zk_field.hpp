@@ -311,6 +311,37 @@ __device__ __forceinline__ void redc_cols(Fe<F> &r, const uint64_t (&T)[2 * F::N
 #pragma unroll
   for (int i = 0; i < N; i++) r.v[i] = o[i];
 }
+// The same reduction in operand-scanning order: digit m_k is formed as soon as column k holds
+// its carry, and its row m_k p_j is added to the 14 later columns at once (independent
+// v_mad_u64_u32, no chain through one accumulator); only mul_lo -> mad -> shift -> add per digit
+// is serial.  Every column ends with the same sum as in redc_cols (the terms are added in another
+// order, all non-negative), so tools/lazy_bounds.py's column bounds hold unchanged.
+template <class F>
+__device__ __forceinline__ void redc_rows(Fe<F> &r, uint64_t (&T)[2 * F::N - 1]) {
+  constexpr int N = F::N;
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const uint32_t m = ((uint32_t)T[k] * F::MINV) & F::MASK;
+#pragma unroll
+    for (int j = 0; j < N; j++) T[k + j] += (uint64_t)m * F::p(j);
+    T[k + 1] += T[k] >> F::RB;  // the low RB bits of T[k] are now zero
+  }
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = N; k < 2 * N - 1; k++) {
+    acc += T[k];
+    r.v[k - N] = (uint32_t)acc & F::MASK;
+    acc >>= F::RB;
+  }
+  r.v[N - 1] = (uint32_t)acc;
+}
+#ifndef ZK_REDC_ROWS
+#define ZK_REDC_ROWS 0  // A/B: 1 = redc_rows in the Karatsuba products below
+#endif
+template <class F>
+__device__ __forceinline__ void redc_k(Fe<F> &r, uint64_t (&T)[2 * F::N - 1]) {
+  if constexpr (ZK_REDC_ROWS) redc_rows(r, T); else redc_cols(r, T);
+}
 // the product / shared-reduction pair with the Karatsuba column sums (14-limb field), the
 // schoolbook ones otherwise
 template <class F>
@@ -318,7 +349,7 @@ __device__ __forceinline__ void fe_mulk(Fe<F> &r, const Fe<F> &a, const Fe<F> &b
   if constexpr (F::N == 14) {
     uint64_t T[2 * F::N - 1];
     kara_cols(T, a, b, false);
-    redc_cols(r, T);
+    redc_k(r, T);
   } else {
     fe_mul(r, a, b);
   }
@@ -329,7 +360,7 @@ __device__ __forceinline__ void fe_mul2k(Fe<F> &r, const Fe<F> &a, const Fe<F> &
     uint64_t T[2 * F::N - 1];
     kara_cols(T, a, b, false);
     kara_cols(T, c, d, true);
-    redc_cols(r, T);
+    redc_k(r, T);
   } else {
     fe_mul2(r, a, b, c, d);
   }

@@ -15,7 +15,8 @@ shift 2 || true
 UNITS=${@:-zk_msm}
 OBJS=""
 for u in $UNITS; do
-  src="$PKG/csrc/$u.hip"; [ -f "$src" ] || src="$PKG/csrc/$u.cpp"
+  SRC=${VARIANT_SRC:-$PKG/csrc}  # VARIANT_SRC: an edited copy of csrc/ (experiments outside the tree)
+  src="$SRC/$u.hip"; [ -f "$src" ] || src="$SRC/$u.cpp"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wno-unused-function \
     -Wno-unused-result $FLAGS -c "$src" -o "$OUT/$u.o"
   OBJS="$OBJS $OUT/$u.o"

@@ -148,6 +148,23 @@ def test_div_by_vanishing(gpu, oracle, curve, n1, n):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("n1,n,zero_top", [(200000, 4096, 100000), (5000, 37, 0), (130, 100, 3), (9000, 64, 4097),
+                                           (70000, 65, 0), (20000, 20000, 0), (12288, 1, 12000),
+                                           (1500000, 4096, 1200000), (600000, 1024, 600000)])
+def test_div_by_vanishing_shapes(gpu, oracle, curve, n1, n, zero_top):
+    """chains of every length mod the wavefront (n < 64, n not a multiple of 64, deg - n < n), and
+    degrees far below the buffer's top (the top-down degree scan skips whole chunks)"""
+    poly = fr(gpu, curve, 97 + n, n1)
+    if zero_top:
+        poly[-zero_top:] = 0
+    eta = fr(gpu, curve, 98, 1)[0]
+    q, r = gpu.div_by_vanishing(curve, poly, n, eta)
+    wq, wr, ok = oracle.div_by_vanishing(curve, poly, n, eta)
+    assert np.array_equal(q, wq) and np.array_equal(r, wr)
+    assert (gpu.quot_by_vanishing(curve, poly, n, eta) is not None) == ok
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_quot_by_vanishing_exact(gpu, curve):
     """(x^n - eta) g(x) / (x^n - eta) = g, remainder zero -- at PLONK-like size 2^16"""
     n, m = 1 << 16, 1 << 16

@@ -506,14 +506,40 @@ __global__ void __launch_bounds__(256) k_powers(int n, int h, const uint64_t *__
 
 // ---------------------------------------------------------------------------- vanishing
 
-__global__ void k_degree(int n, const uint64_t *__restrict__ a, int *__restrict__ deg) {
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  int best = -1;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)n; i += stride) {
-    const uint64_t *x = a + i * 4;
-    if (x[0] | x[1] | x[2] | x[3]) best = (int)i;
+// degree of a[0, n) (-1: zero polynomial), scanned from the top by a grid of DEG_GRID blocks:
+// round k has block b take the (k DEG_GRID + b)-th chunk of DEG_CHUNK coefficients counted from
+// the end, and every block stops once a nonzero coefficient was found at or above its next chunk
+// -- the usual polynomial, nonzero near its top, costs one round (DEG_GRID x 32 KiB) instead of
+// the whole array.  (A grid of one block per chunk scans everything: all of its blocks are
+// resident before the top one finishes -- 0.198 ms at 2^23.6 coefficients, profiles/r06r_*.)
+constexpr int DEG_CHUNK = 1024, DEG_GRID = 256;
+__global__ void __launch_bounds__(256) k_degree(int n, const uint64_t *__restrict__ a, int *__restrict__ deg) {
+  const long long nchunk = ((long long)n + DEG_CHUNK - 1) / DEG_CHUNK;
+  const uint4 *x = reinterpret_cast<const uint4 *>(a);
+  __shared__ int stop;
+  for (long long c = nchunk - 1 - (long long)blockIdx.x; c >= 0; c -= gridDim.x) {
+    const long long lo = c * DEG_CHUNK;
+    if (threadIdx.x == 0) stop = __hip_atomic_load(deg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= lo;
+    __syncthreads();
+    if (stop) return;  // one value for the whole block
+    const long long hi = min((long long)n, lo + DEG_CHUNK);
+    int best = -1;
+    uint4 u[DEG_CHUNK / 256][2];
+#pragma unroll
+    for (int k = 0; k < DEG_CHUNK / 256; k++) {  // every load of the chunk in flight at once
+      const long long i = lo + (long long)threadIdx.x + 256 * k;
+      u[k][0] = i < hi ? x[2 * i] : make_uint4(0, 0, 0, 0);
+      u[k][1] = i < hi ? x[2 * i + 1] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < DEG_CHUNK / 256; k++)
+      if (u[k][0].x | u[k][0].y | u[k][0].z | u[k][0].w | u[k][1].x | u[k][1].y | u[k][1].z | u[k][1].w)
+        best = (int)(lo + (long long)threadIdx.x + 256 * k);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));  // one atomic per wavefront
+    if ((threadIdx.x & 63) == 0 && best >= 0) atomicMax(deg, best);
+    __syncthreads();  // every thread has read `stop` before thread 0 rewrites it
   }
-  if (best >= 0) atomicMax(deg, best);
 }
 // quotient by x^n - eta (deg_p >= n): q_j = a_{j+n} + eta q_{j+n}, one lane per residue
 // class j mod n walking its chain from the top (poly_mont.c:360-372 / 337-347)
@@ -536,6 +562,73 @@ __global__ void __launch_bounds__(256) k_vanish_quot(int deg, int n, const uint6
     fe_add(q, ai, t);
     st(quot, (size_t)j, q);
   }
+}
+// The same chains fused with the remainder, on the LDS-staged nontemporal 1-KiB runs of the Fr
+// ops: wavefront w owns residues [e0, e0 + 64) and walks their chains top-down in lockstep -- at
+// step s its lanes read a[e0 + s n + n ..] and write quot[e0 + s n ..], each a contiguous run
+// (lanes whose chain has not started read past the degree, i.e. zeros, and keep q = 0, so no
+// masking); after step 0 each lane holds q_rho and writes rem_rho = a_rho + eta q_rho (q_rho = 0
+// for rho > deg - n, where the remainder is a_rho itself).  Every quotient index <= deg - n and
+// every remainder index < n is written; the host clears only the buffers' tails.
+// STAGED = false (the default, see div_vanishing_t): the same fused chains with per-lane 32-B accesses
+template <class F, bool STAGED = true>
+__global__ void __launch_bounds__(256) k_vanish_fused(int deg, int n, const uint64_t *__restrict__ a, U256 eta,
+                                                      uint64_t *__restrict__ quot, uint64_t *__restrict__ rem) {
+  __shared__ uint4 lds[4][128];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t e0 = (size_t)blockIdx.x * 256 + (size_t)wave * 64;
+  if (e0 >= (size_t)n) return;  // wave-uniform
+  const size_t top = (size_t)(deg - n), N = (size_t)n;
+  const size_t rlim = (size_t)min((size_t)n, e0 + 64);  // residues of this wave: [e0, rlim)
+  Fe<F> e, er, q;
+  ld_const(er, eta);
+  fe_to_int(e, er);
+  fe_zero(q);
+  if constexpr (!STAGED) {
+    const size_t rho = e0 + lane;
+    if (rho >= N) return;
+    if (rho <= top) {
+      for (size_t j = rho + ((top - rho) / N) * N;; j -= N) {
+        Fe<F> ai, t;
+        ld(ai, a, j + N);
+        fe_mul(t, e, q);
+        fe_add(q, ai, t);
+        st(quot, j, q);
+        if (j < N) break;
+      }
+    }
+    Fe<F> ar, t, r;
+    ld(ar, a, rho);
+    fe_mul(t, e, q);
+    fe_add(r, ar, t);
+    st(rem, rho, r);
+    return;
+  }
+  // every load is independent of the products: the remainder's runs are fetched first and each
+  // step's runs one step ahead (registers), so a wavefront keeps loads in flight through its chain
+  Runs rr, rn;
+  fetch_runs<true>(rr, a, e0, rlim, lane);
+  if (e0 <= top) {
+    const size_t lim = (size_t)deg + 1;
+    size_t s = (top - e0) / N;  // chain length of residue e0 (the longest) - 1
+    fetch_runs<true>(rn, a, e0 + s * N + N, lim, lane);
+    for (;;) {
+      const size_t j0 = e0 + s * N;
+      Fe<F> ai, t;
+      place_runs(ai, rn, lds[wave], lane);
+      if (s > 0) fetch_runs<true>(rn, a, j0, lim, lane);  // step s - 1 reads a[j0 - N + N ..]
+      fe_mul(t, e, q);
+      fe_add(q, ai, t);
+      st_staged<F, true>(quot, j0, min(top + 1, rlim + s * N), q, lds[wave], lane);
+      if (s == 0) break;
+      s--;
+    }
+  }
+  Fe<F> ar, t, r;
+  place_runs(ar, rr, lds[wave], lane);
+  fe_mul(t, e, q);
+  fe_add(r, ar, t);
+  st_staged<F, true>(rem, e0, rlim, r, lds[wave], lane);
 }
 template <class F>
 __global__ void __launch_bounds__(256) k_vanish_rem(int deg, int n, const uint64_t *__restrict__ a,
@@ -857,7 +950,8 @@ static int div_vanishing_t(Device &dev, int n1, const uint64_t *src, int n, cons
   int *ddeg = dev.arena.take<int>(1);
   ZK_CHECK(hipMemsetAsync(ddeg, 0xff, 4, st));  // -1
   if (N1) {
-    hipLaunchKernelGGL(k_degree, dim3(grid_for(N1)), dim3(256), 0, st, n1, da, ddeg);
+    hipLaunchKernelGGL(k_degree, dim3((unsigned)std::min<size_t>(DEG_GRID, (N1 + DEG_CHUNK - 1) / DEG_CHUNK)), dim3(256), 0,
+                       st, n1, da, ddeg);
     ZK_CHECK(hipGetLastError());
   }
   int *hdeg = reinterpret_cast<int *>(dev.host_staging(4));
@@ -866,9 +960,15 @@ static int div_vanishing_t(Device &dev, int n1, const uint64_t *src, int n, cons
   const int deg = *hdeg;
   ZK_REQUIRE(nquot >= deg - n + 1, "poly_div_by_vanishing: quotient buffer too small");  // poly_mont.c:328
   ZK_REQUIRE(!want_rem || nrem >= n, "poly_div_by_vanishing: remainder buffer too small");  // :329
-  if (nquot > 0) ZK_CHECK(hipMemsetAsync(dq, 0, (size_t)nquot * 32, st));
-  if (NR) ZK_CHECK(hipMemsetAsync(dr, 0, NR * 32, st));
   const U256 e = load_u256(eta);
+  static const bool legacy = [] {  // ZK_VANISH_LEGACY=1: the round-5 kernels (A/B hook, read once)
+    const char *v = getenv("ZK_VANISH_LEGACY");
+    return v && v[0] == '1';
+  }();
+  // the fused kernel writes quot[0, deg - n] and rem[0, n): only the tails are cleared
+  const size_t qw = (deg >= n && !legacy) ? (size_t)(deg - n + 1) : 0, rw = (deg >= n && !legacy) ? (size_t)n : 0;
+  if ((size_t)nquot > qw) ZK_CHECK(hipMemsetAsync(dq + qw * 4, 0, ((size_t)nquot - qw) * 32, st));
+  if (NR > rw) ZK_CHECK(hipMemsetAsync(dr + rw * 4, 0, (NR - rw) * 32, st));
   if (deg < n) {  // quotient 0, remainder = p (poly_mont.c:332-341)
     if (deg >= 0) {
       ZK_REQUIRE(NR >= (size_t)deg + 1, "poly_div_by_vanishing: remainder buffer too small");
@@ -876,9 +976,20 @@ static int div_vanishing_t(Device &dev, int n1, const uint64_t *src, int n, cons
     }
   } else {
     using F = typename Cfg::Fd;
-    hipLaunchKernelGGL(k_vanish_quot<F>, dim3(div_up(n, 256)), dim3(256), 0, st, deg, n, da, e, dq);
-    ZK_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(k_vanish_rem<F>, dim3(div_up(n, 256)), dim3(256), 0, st, deg, n, da, dq, e, dr);
+    if (legacy) {
+      hipLaunchKernelGGL(k_vanish_quot<F>, dim3(div_up(n, 256)), dim3(256), 0, st, deg, n, da, e, dq);
+      ZK_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(k_vanish_rem<F>, dim3(div_up(n, 256)), dim3(256), 0, st, deg, n, da, dq, e, dr);
+    } else {
+      // per-lane 32-B accesses by default: 0.186 vs 0.197 ms for the LDS-staged runs at deg 3 x 2^22
+      // (profiles/r06r_vanish_prof.txt); ZK_VANISH_STAGED=1 selects those (A/B hook, read once)
+      static const bool staged = [] {
+        const char *v = getenv("ZK_VANISH_STAGED");
+        return v && v[0] == '1';
+      }();
+      if (staged) hipLaunchKernelGGL((k_vanish_fused<F, true>), dim3(div_up(n, 256)), dim3(256), 0, st, deg, n, da, e, dq, dr);
+      else hipLaunchKernelGGL((k_vanish_fused<F, false>), dim3(div_up(n, 256)), dim3(256), 0, st, deg, n, da, e, dq, dr);
+    }
     ZK_CHECK(hipGetLastError());
   }
   sg.back(quot, dq, (size_t)nquot);

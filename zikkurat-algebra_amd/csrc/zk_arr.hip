@@ -350,6 +350,103 @@ __global__ void __launch_bounds__(256) k_inv_chunks(int op, int n, int CHK, cons
   }
 }
 
+// The strided chunks with TWO interleaved chains per lane (round 6, ZK_INV_ILP=0 restores the one-
+// chain kernel): elements k = 0, 2, 4, ... and k = 1, 3, 5, ... of a lane's chunk keep separate running
+// products, so every step issues two independent products where the one-chain kernel waits for the
+// previous product's last column; the two totals share ONE inversion (P0 P1)^-1, split as
+// P0^-1 = (P0 P1)^-1 P1 and P1^-1 = (P0 P1)^-1 P0 (two products per lane).  A lane with an odd count
+// pads chain 1 with a 1 (its product runs, its load and store do not).  Scratch holds each element's
+// running product within its own chain.
+template <class F>
+__device__ __forceinline__ void fe_sel(Fe<F> &r, bool c, const Fe<F> &a, const Fe<F> &b) {
+#pragma unroll
+  for (int i = 0; i < F::N; i++) r.v[i] = c ? a.v[i] : b.v[i];
+}
+// Straight-line steps: every load and store of a step is unconditional (a lane past its count
+// re-reads / re-writes its element k0 with the same value), so no branch splits the step and the
+// compiler's wait counts let the step's loads fly together (a conditional load or store makes it
+// wait for everything outstanding where the paths merge).
+template <class F>
+__global__ void __launch_bounds__(256) k_inv_chunks2(int op, int n, int CHK, const uint64_t *__restrict__ a,
+                                                     const uint64_t *__restrict__ x, uint64_t *__restrict__ scratch,
+                                                     uint64_t *tgt, uint32_t *zflag, int lanes) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t T = (size_t)lanes;
+  if (t >= T || t >= (size_t)n) return;
+  const size_t left = ((size_t)n - t + T - 1) / T;
+  const size_t cnt = left < (size_t)CHK ? left : (size_t)CHK;
+  const size_t pairs = (cnt + 1) / 2;
+  const bool div = op == ARR_DIV;
+  Fe<F> P0, P1, one;
+  fe_one(one);
+  P0 = one;
+  P1 = one;
+  bool zero = false;
+  for (size_t j = 0; j < pairs; j++) {
+    const size_t k0 = 2 * j, i0 = t + k0 * T;
+    const bool has1 = k0 + 1 < cnt;
+    const size_t i1 = has1 ? i0 + T : i0;
+    Fe<F> v0, v1, w0, w1, u1, q0, q1;
+    ld(v0, x, i0);
+    ld(v1, x, i1);
+    zero |= fe_is_zero(v0);
+    zero |= fe_is_zero(v1);
+    fe_to_int(w0, v0);
+    fe_to_int(u1, v1);
+    fe_sel(w1, has1, u1, one);
+    fe_mul(q0, P0, w0);
+    fe_mul(q1, P1, w1);
+    P0 = q0;
+    P1 = q1;
+    Fe<F> s1;
+    fe_sel(s1, has1, P1, P0);
+    st(scratch, i0, P0);
+    st(scratch, i1, s1);
+  }
+  if (zero) atomicOr(zflag, 1u);
+  Fe<F> P, inv, inv0, inv1;
+  fe_mul(P, P0, P1);
+  fe_inv_sg(inv, P);
+  fe_mul(inv0, inv, P1);
+  fe_mul(inv1, inv, P0);
+  for (size_t j = pairs; j-- > 0;) {
+    const size_t k0 = 2 * j, i0 = t + k0 * T;
+    const bool has1 = k0 + 1 < cnt;
+    const size_t i1 = has1 ? i0 + T : i0;
+    // the chains' previous elements k0 - 2 and k0 - 1 (any valid index when j = 0: unused)
+    const size_t ip0 = j > 0 ? i0 - 2 * T : i0, ip1 = j > 0 ? i0 - T : i0;
+    Fe<F> p0, p1, o0, o1, v0, v1, w0, w1, u1, q0, q1, a0, a1, r0, r1, e0, e1;
+    ld(e0, scratch, ip0);
+    ld(e1, scratch, ip1);
+    ld(v0, x, i0);
+    ld(v1, x, i1);
+    ld(a0, a, div ? i0 : 0);  // a is the dividend (ARR_DIV) or unused: then element 0 of x's buffer
+    ld(a1, a, div ? i1 : 0);
+    fe_sel(p0, j > 0, e0, one);
+    fe_sel(p1, j > 0, e1, one);
+    fe_to_int(w0, v0);
+    fe_to_int(u1, v1);
+    fe_sel(w1, has1, u1, one);
+    fe_mul(o0, inv0, p0);  // 1/x_(k0) (internal)
+    fe_mul(o1, inv1, p1);  // 1/x_(k0 + 1)
+    fe_mul(q0, inv0, w0);
+    fe_mul(q1, inv1, w1);
+    inv0 = q0;
+    inv1 = q1;
+    if (div) {
+      fe_mul(r0, o0, a0);  // (1/x) R' * a R / R' = (a/x) R
+      fe_mul(r1, o1, a1);
+    } else {
+      fe_to_ref(r0, o0);
+      fe_to_ref(r1, o1);
+    }
+    Fe<F> s1;
+    fe_sel(s1, has1, r1, r0);
+    st(tgt, i0, r0);
+    st(tgt, i1, s1);
+  }
+}
+
 __global__ void k_zero_if_flag(int n, uint64_t *__restrict__ tgt, const uint32_t *__restrict__ zflag) {
   if (*zflag == 0) return;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -832,7 +929,13 @@ static void arr_op_t(Device &dev, int op, int n, const uint64_t *a, const uint64
       const dim3 ig(div_up(lanes, 256)), ib(256);
       const uint64_t *xs = op == ARR_DIV ? db : da;
       const U256 pm2 = p_minus_2<Cfg>();
-      if (sg && strided)
+      static const bool ilp2 = [] {
+        const char *e = getenv("ZK_INV_ILP");
+        return !(e && e[0] == '0');
+      }();
+      if (sg && strided && ilp2)
+        hipLaunchKernelGGL(k_inv_chunks2<F>, ig, ib, 0, st, op, n, CHK, op == ARR_DIV ? da : xs, xs, scratch, dt, flag, (int)lanes);
+      else if (sg && strided)
         hipLaunchKernelGGL((k_inv_chunks<F, true, true>), ig, ib, 0, st, op, n, CHK, da, xs, scratch, dt, pm2, flag, (int)lanes);
       else if (sg)
         hipLaunchKernelGGL((k_inv_chunks<F, true, false>), ig, ib, 0, st, op, n, CHK, da, xs, scratch, dt, pm2, flag, (int)lanes);

@@ -107,7 +107,25 @@ enum { MODE_PROJ_TO_AFF = 0, MODE_XYZZ_TO_PROJ = 1, MODE_JAC_TO_AFF = 2 };
 
 // Round 6: the chunk of lane t is the strided set {t, t + T, ...} (T = lanes, as k_inv_chunks):
 // neighbouring lanes touch neighbouring point rows.  STRIDED = false: CHK consecutive points.
-template <class C, int MODE, bool SG = true, bool STRIDED = true>
+// canonical reference-form words of a (internal form), or `alt` where !keep, stored as 16-B runs
+template <class F>
+__device__ __forceinline__ void st_ref_or(uint64_t *p, const Fe<F> &a, bool keep, const uint32_t (&alt)[F::NW]) {
+  Fe<F> t;
+  fe_to_ref(t, a);
+  fe_canon(t);
+  uint32_t w[F::NW];
+  fe_pack(w, t);
+#pragma unroll
+  for (int i = 0; i < F::NW; i++) w[i] = keep ? w[i] : alt[i];
+  uint4 *q = reinterpret_cast<uint4 *>(p);
+#pragma unroll
+  for (int i = 0; i < F::NW / 4; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+// BF (round 6, default; ZK_NORM_BF=0 restores the branches): every step branch-free -- the points at
+// infinity take the factor 1 and have their output rows selected word by word, and every load and
+// store is unconditional, so no path merge inside the loop makes the compiler wait for all
+// outstanding memory (the Fr inversion measured the same effect, profiles/r06v_inv_ilp_ab.txt).
+template <class C, int MODE, bool SG = true, bool STRIDED = true, bool BF = true>
 __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void *__restrict__ srcv,
                                                      uint64_t *__restrict__ scratch, uint64_t *__restrict__ tgt,
                                                      W6 pm2, int bitrev_m, int lanes) {
@@ -129,12 +147,20 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
     }
     return !fe_is_zero(d);
   };
-  Fe<F> P;
+  Fe<F> P, one_int;
   fe_one(P);
+  fe_one(one_int);
   for (size_t k = 0; k < cnt; k++) {
     const size_t i = i0 + k * T;
     Fe<F> d, q;
-    if (den(i, d)) {
+    if constexpr (BF) {
+      const bool fin = den(i, d);
+      Fe<F> f;
+#pragma unroll
+      for (int l = 0; l < F::N; l++) f.v[l] = fin ? d.v[l] : one_int.v[l];
+      fe_mul(q, P, f);
+      P = q;
+    } else if (den(i, d)) {
       fe_mul(q, P, d);
       P = q;
     }
@@ -143,8 +169,64 @@ __global__ void __launch_bounds__(256) k_norm_chunks(int n, int CHK, const void 
   Fe<F> inv;
   if (SG) fe_inv_sg(inv, P);  // divsteps (zk_inv.hpp); Fermat with ZK_INV_SG=0
   else fe_pow_words<F, NP>(inv, P, pm2);
-  Fe<F> one_int;
-  fe_one(one_int);
+  if constexpr (BF) {
+    uint32_t ones[F::NW], zeros[F::NW], oneref[F::NW];
+    {
+      Fe<F> t;
+      fe_to_ref(t, one_int);
+      fe_canon(t);
+      fe_pack(oneref, t);
+    }
+#pragma unroll
+    for (int l = 0; l < F::NW; l++) { ones[l] = ~0u; zeros[l] = 0; }
+    for (size_t kk = cnt; kk-- > 0;) {
+      const size_t i = i0 + kk * T;
+      Fe<F> d, e, prev, f, dinv, q;
+      const bool fin = den(i, d);
+      size_t o = i;
+      if (MODE == MODE_XYZZ_TO_PROJ && bitrev_m > 0)
+        o = (size_t)(__builtin_bitreverse32((uint32_t)i) >> (32 - bitrev_m));
+      fe_load_ref(e, scratch + (kk > 0 ? i - T : i) * NP);
+#pragma unroll
+      for (int l = 0; l < F::N; l++) {
+        prev.v[l] = kk > 0 ? e.v[l] : one_int.v[l];
+        f.v[l] = fin ? d.v[l] : one_int.v[l];
+      }
+      fe_mul(dinv, inv, prev);  // 1 / d_i
+      fe_mul(q, inv, f);
+      inv = q;
+      if (MODE == MODE_PROJ_TO_AFF || MODE == MODE_JAC_TO_AFF) {
+        Fe<F> X, Y, x, y;
+        ld_int(X, srcp + i * 3 * NP);
+        ld_int(Y, srcp + i * 3 * NP + NP);
+        if (MODE == MODE_PROJ_TO_AFF) {
+          fe_mul(x, X, dinv);
+          fe_mul(y, Y, dinv);
+        } else {
+          Fe<F> d2, d3;
+          fe_sqr(d2, dinv);
+          fe_mul(d3, d2, dinv);
+          fe_mul(x, X, d2);
+          fe_mul(y, Y, d3);
+        }
+        st_ref_or(tgt + o * 2 * NP, x, fin, ones);  // infinity: all-ones row, G1_proj.c:134-138
+        st_ref_or(tgt + o * 2 * NP + NP, y, fin, ones);
+      } else {
+        Xyzz<F> p;
+        xyzz_load(p, srcx + i * xw<F>());
+        Fe<F> iz, iz2, x, y;
+        fe_mul(iz, p.ZZ, dinv);  // ZZ / ZZZ = 1/Z
+        fe_sqr(iz2, iz);         // 1/ZZ
+        fe_mul(x, p.X, iz2);
+        fe_mul(y, p.Y, dinv);
+        uint64_t *qo = tgt + o * 3 * NP;
+        st_ref_or(qo, x, fin, zeros);  // infinity: (0 : 1 : 0)
+        st_ref_or(qo + NP, y, fin, oneref);
+        st_ref_or(qo + 2 * NP, one_int, fin, zeros);
+      }
+    }
+    return;
+  }
   for (size_t kk = cnt; kk-- > 0;) {
     const size_t i = i0 + kk * T;
     Fe<F> d;
@@ -1262,20 +1344,31 @@ static bool inv_strided() {
   }();
   return on;
 }
+// ZK_NORM_BF=0: k_norm_chunks with the round-6 branches (A/B hook, read once; default branch-free)
+static bool norm_bf() {
+  static const bool on = [] {
+    const char *e = getenv("ZK_NORM_BF");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 template <class C, int MODE>
 static void launch_norm(hipStream_t st, int n, int chk, const void *src, uint64_t *scratch, uint64_t *tgt, W6 pm2,
                         int bitrev_m) {
   const size_t lanes = ((size_t)n + chk - 1) / chk;
   const dim3 grid(div_up(lanes, 256));
-  if (inv_sg() && inv_strided())
-    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true, true>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2,
+  if (inv_sg() && inv_strided() && norm_bf())
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true, true, true>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2,
                        bitrev_m, (int)lanes);
+  else if (inv_sg() && inv_strided())
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true, true, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt,
+                       pm2, bitrev_m, (int)lanes);
   else if (inv_sg())
-    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2,
-                       bitrev_m, (int)lanes);
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, true, false, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt,
+                       pm2, bitrev_m, (int)lanes);
   else
-    hipLaunchKernelGGL((k_norm_chunks<C, MODE, false, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt, pm2,
-                       bitrev_m, (int)lanes);
+    hipLaunchKernelGGL((k_norm_chunks<C, MODE, false, false, false>), grid, dim3(256), 0, st, n, chk, src, scratch, tgt,
+                       pm2, bitrev_m, (int)lanes);
   ZK_CHECK(hipGetLastError());
 }
 static int norm_chk(size_t N) {

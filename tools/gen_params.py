@@ -110,6 +110,12 @@ def unsat_block(name, p):
     out.append(f"#define ZK_{P}_S62_P {{ {vals} }}")
     out.append(f"#define ZK_{P}_S62_PINV 0x{pow(p, -1, 1 << 62):016x}ull")
     out.append(f"#define ZK_{P}_S62_BATCHES {-(-steps // 62)}")
+    # the same in 60-bit limbs for batches of 2 x 30 divsteps in 32-bit arithmetic (zk_inv.hpp B = 60)
+    L60 = (nbits + 2 + 59) // 60
+    vals = ", ".join("%dll" % ((p >> (60 * i)) & ((1 << 60) - 1)) for i in range(L60))
+    out.append(f"#define ZK_{P}_S60_L {L60}")
+    out.append(f"#define ZK_{P}_S60_P {{ {vals} }}")
+    out.append(f"#define ZK_{P}_S60_BATCHES {-(-steps // 60)}")
     return out
 
 

@@ -58,6 +58,10 @@ namespace zk {
     static constexpr uint64_t S62_PINV = PFX##_S62_PINV;                              \
     __host__ __device__ static constexpr int64_t s62p(int i) {                          \
       constexpr int64_t v_[] = PFX##_S62_P; return v_[i]; }                           \
+    static constexpr int S60_L = PFX##_S60_L;           /* 60-bit limbs, 2 x 30 steps */ \
+    static constexpr int S60_NB = PFX##_S60_BATCHES;                                   \
+    __host__ __device__ static constexpr int64_t s60p(int i) {                          \
+      constexpr int64_t v_[] = PFX##_S60_P; return v_[i]; }                           \
   };
 
 ZK_DEFINE_FIELD(BN_Fp, ZK_BN128_FP)
@@ -680,6 +684,9 @@ __device__ __forceinline__ void fe_store_ref(uint64_t *__restrict__ p, const Fe<
 // x^-1 R' (< 2p).  canon(a) = x R' mod p as an integer; b = (x R')^-1 mod p by divsteps; one product
 // by R'^3 gives x^-1 R'.  a = 0 gives 0.  ~18 / 12 batches of 62 divsteps (381- / 255-bit fields)
 // instead of a 489 / 323-product Fermat chain (round 6).
+#ifndef ZK_INV_DS30
+#define ZK_INV_DS30 1  // 60-bit limbs, batches of 2 x 30 divsteps in 32-bit arithmetic; 0: 62 in 64-bit
+#endif
 template <class F>
 __device__ __forceinline__ void fe_inv_sg(Fe<F> &r, const Fe<F> &a) {
   Fe<F> c = a;
@@ -689,10 +696,17 @@ __device__ __forceinline__ void fe_inv_sg(Fe<F> &r, const Fe<F> &a) {
   uint64_t x[F::N64], y[F::N64];
 #pragma unroll
   for (int i = 0; i < F::N64; i++) x[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+#if ZK_INV_DS30
+  int64_t P[F::S60_L];
+#pragma unroll
+  for (int i = 0; i < F::S60_L; i++) P[i] = F::s60p(i);
+  sg_inverse_words<F::S60_L, F::S60_NB, 60>(y, x, F::N64, P, F::S62_PINV);
+#else
   int64_t P[F::S62_L];
 #pragma unroll
   for (int i = 0; i < F::S62_L; i++) P[i] = F::s62p(i);
   sg_inverse_words<F::S62_L, F::S62_NB>(y, x, F::N64, P, F::S62_PINV);
+#endif
 #pragma unroll
   for (int i = 0; i < F::N64; i++) {
     w[2 * i] = (uint32_t)y[i];
